@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: Mvoxels/s per output frame of the LK optical-flow hot path on MI355X.
+
+Metric (BASELINE.json): "Mvoxels/s per frame-pair (and HBM GB/s fraction) at
+1/2/4/8 MI355X".  One step = one pass of the hot path (calc_flow3D,
+src/Python/calc_flow.py:175-360) over one output frame: the 2*rt+1 input
+frames are resident in HBM when the timed region starts; the step runs the
+five-kernel pipeline through the C-ABI (of3d_plan_execute) and leaves
+vx, vy, vz (fp64) and rel (fp32) in HBM.
+
+Default workload = BASELINE.json configs[1] (c2): 3D 256x256x64, 13 frames,
+xyzSig=2 tSig=2 wSig=5, fp64.  --config c3 selects configs[2].
+N > 1 (torch.distributed.run, one rank per GPU): frame replicas — every rank
+computes its own output frame (calc_flow.py:512 marks output frames as the
+independent axis); no data-path collective; value = all ranks' voxels / max
+rank time.  Rank 0 prints ONE JSON line.
+
+Roofline: the dominant kernel's average duration from HIP events recorded on
+the launch stream over the timed region (of3d_plan_set_timing ring), with its
+algorithmic bytes and fp64 VALU op count; HBM traffic
+from the committed rocprofv3 PMC summary (profiles/) when present.
+cpu_baseline: the oracle (oracle/cpu_ref.py, scipy correlate1d + LAPACK cgeev
+as the reference uses) on one thread, rank 0 at N=1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    # name: (Nt, Nz, Ny, Nx, xyzSig, tSig, wSig, description)
+    "c2": (13, 64, 256, 256, 2, 2, 5, "configs[1]: 3D OneTif 256x256x64 x13 frames (tSig=2), xyzSig=2 wSig=5, fp64"),
+    "c3": (19, 128, 512, 512, 2, 3, 7, "configs[2]: 3D 512x512x128 x19 frames (tSig=3), xyzSig=2 wSig=7, fp64"),
+}
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOP/s fp64 vector counts an FMA as 2; add/mul issue at half
+
+
+def synthetic_frames(nt, nz, ny, nx, seed):
+    """uint16 stack: translated separable sinusoids + bounded noise."""
+    rng = np.random.default_rng(seed)
+    z = np.arange(nz, dtype=np.float64)[:, None, None]
+    y = np.arange(ny, dtype=np.float64)[None, :, None]
+    x = np.arange(nx, dtype=np.float64)[None, None, :]
+    k = rng.uniform(2 * np.pi / 24, 2 * np.pi / 6, size=(3, 3))
+    ph = rng.uniform(0, 2 * np.pi, size=(3, 3))
+    vel = (0.3, -0.2, -0.1)  # (vx, vy, vz) voxels/frame
+    out = np.empty((nt, nz, ny, nx), np.uint16)
+    for t in range(nt):
+        s = np.zeros((nz, ny, nx))
+        for q in range(3):
+            s = s + (np.sin(k[q, 0] * (x - vel[0] * t) + ph[q, 0]) * np.sin(k[q, 1] * (y - vel[1] * t) + ph[q, 1])
+                     * np.sin(k[q, 2] * (z - vel[2] * t) + ph[q, 2]))
+        noise = rng.integers(-8, 9, size=(nz, ny, nx))
+        out[t] = np.clip(1000 + 300 * s + noise, 0, 65535).astype(np.uint16)
+    return out
+
+
+def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane):
+    """Algorithmic HBM bytes and fp64 VALU ops per launch of each stage.
+
+    Bytes are the compulsory reads + writes of the stage's own inputs/outputs
+    (each element once); ops count every add and multiply of the scipy-order
+    passes (C(r) = 1 + 3r per symmetric/antisymmetric output)."""
+    C = lambda r: 1 + 3 * r
+    return {
+        "grad_xy": {"bytes": (nt_win * 2 + 4 * 8) * nb * plane,
+                    "ops": (C(rt) + C(rd) * 2 + C(rs) + C(rd) * 2 + C(rs) * 2) * nb * plane},
+        "grad_z": {"bytes": (4 * 8 + 4 * 8) * ng * plane, "ops": (C(rd) * 2 + C(rs) * 2) * ng * plane},
+        "prod_wy": {"bytes": (4 * 8 + 9 * 8) * ng * plane, "ops": (9 + 9 * C(rw)) * ng * plane},
+        "wx": {"bytes": (9 * 8 + 9 * 8) * ng * plane, "ops": 9 * C(rw) * ng * plane},
+        "wz_solve": {"bytes": (9 * 8 + 3 * 8 + 4) * no * plane, "ops": (9 * C(rw) + 65 + 50) * no * plane},
+    }
+
+
+def load_pmc_traffic(kernel, cfg):
+    path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(frames, s, t, w, budget_s):
+    """Time the oracle (scipy correlate1d + LAPACK cgeev, the reference's primitives) on 1 thread."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cpu_ref
+
+    nt, nz, ny, nx = frames.shape
+    with threadpool_limits(limits=1):
+        # bounded sample: whole frame if it fits the budget estimate, else a z-subvolume
+        sub_nz = nz
+        est = nz * ny * nx / 0.25e6  # ~0.25 Mvox/s on one core
+        if est > budget_s:
+            sub_nz = max(8, int(nz * budget_s / est))
+        sample = frames[:, :sub_nz]
+        t0 = time.perf_counter()
+        cpu_ref.calc_flow3D(sample, s, t, w, backend="scipy")
+        dt = time.perf_counter() - t0
+    vox = sub_nz * ny * nx
+    what = "full frame" if sub_nz == nz else f"z-subvolume {sub_nz} of {nz} planes"
+    return {"value": round(vox / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+            "sample": f"{what} ({sub_nz}x{ny}x{nx} voxels, {nt} frames): oracle/cpu_ref.py calc_flow3D with "
+                      f"scipy.ndimage.correlate1d + numpy.linalg.eigvals(complex64), 1 thread, {dt:.2f} s",
+            "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
+
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd import _lib, make_taps, radii
+
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    rd, rs, rt, rw = radii(s, t, w)
+    nwin = 2 * rt + 1
+    frames = synthetic_frames(nt, nz, ny, nx, seed=20260206 + 2 + rank)
+    c = nt // 2
+    win = np.ascontiguousarray(frames[c - rt:c + rt + 1])
+    d_in = torch.from_numpy(win.view(np.int16)).to(dev)
+    vox = nz * ny * nx
+    d_vx = torch.empty(vox, dtype=torch.float64, device=dev)
+    d_vy = torch.empty_like(d_vx)
+    d_vz = torch.empty_like(d_vx)
+    d_rel = torch.empty(vox, dtype=torch.float32, device=dev)
+
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=local_rank, timing=max(args.steps, 1))
+    fptrs = [d_in[i].data_ptr() for i in range(nwin)]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        plan.execute(fptrs, _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(), d_vz.data_ptr(),
+                     d_rel.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    try:
+        plan.stage_times()  # drop warmup records
+    except RuntimeError:
+        pass
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = plan.stage_times()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # sanity: finite outputs
+    finite = bool(torch.isfinite(d_vx).all().item())
+
+    if rank == 0:
+        ms_step = elapsed / args.steps * 1e3
+        value = world * vox * args.steps / elapsed / 1e6
+        plane = ny * nx
+        model = stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, plane)
+        dom = max(stages, key=stages.get)
+        dom_ms = stages[dom]
+        ach = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
+        traffic = load_pmc_traffic(dom, args.config)
+        frame_bytes = (nwin * 2 + 3 * 8 + 4) * vox  # B = nt*s_in + 3*s_v + s_rel
+        frame_ms = sum(stages.values())
+        roof = {
+            "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_launch": model[dom]["bytes"], "avg_launch_ms": round(dom_ms, 5),
+            "valu_fp64_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
+            "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+            "stage_ms": {k: round(v, 5) for k, v in stages.items()},
+            "frame": {"bytes_per_voxel": nwin * 2 + 3 * 8 + 4, "device_ms": round(frame_ms, 4),
+                      "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
+                      "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        }
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(frames, s, t, w, args.cpu_budget)
+        line = {
+            "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
+            "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
+                       "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
+                       "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

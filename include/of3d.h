@@ -1,0 +1,150 @@
+/*
+ * of3d.h — C-ABI of the MI355X (gfx950) Lucas–Kanade optical-flow engine.
+ *
+ * Drop-in boundary for the hot path of ScientistRachel/OpticalFlow3D_dev:
+ *   calc_flow3D(images, xyzSig, tSig, wSig) -> (vx, vy, vz, rel)   src/Python/calc_flow.py:175-360
+ *   calc_flow2D(images, xySig,  tSig, wSig) -> (vx, vy, rel)       src/Python/calc_flow.py:18-173
+ * The reference has no FFI of its own (pure NumPy/SciPy); the Python host in
+ * opticalflow3d_dev_amd/calc_flow.py keeps those signatures and binds these
+ * entry points with ctypes (binding shown in INTEGRATION.md).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Arrays are C-ordered, x fastest:
+ *    images (Nt, Nz, Ny, Nx) / (Nt, Ny, Nx); outputs (Nz, Ny, Nx) / (Ny, Nx).
+ *  - Host entry points (of3d_flow3d / of3d_flow2d): the caller owns every host
+ *    buffer; the library owns device memory (cached per shape+taps).
+ *  - Device entry point (of3d_plan_execute): every pointer is device memory,
+ *    work is enqueued on the given HIP stream (NULL = the plan's stream) and
+ *    the call returns without synchronising.
+ *  - Return 0 on success; non-zero = error, text in of3d_last_error()
+ *    (thread-local).  The Python host maps the reference's argument checks
+ *    (calc_flow.py:212-222) to SystemExit itself before calling in.
+ *  - Taps are passed explicitly (full odd-length vectors, centre at index r),
+ *    computed by the caller exactly as calc_flow.py:230-267 does; the library
+ *    checks (anti)symmetry like scipy's NI_Correlate1D and uses the symmetric
+ *    summation order (bit-exact with scipy.ndimage.correlate1d).
+ */
+#ifndef OF3D_H
+#define OF3D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OF3D_VERSION 10000 /* 1.0.0 */
+
+/* element type of the input image stack (reference accepts any real dtype and
+ * casts with images.astype(np.float64), calc_flow.py:225 / :67) */
+enum of3d_dtype {
+    OF3D_U8 = 1,
+    OF3D_U16 = 2,
+    OF3D_I16 = 3,
+    OF3D_U32 = 4,
+    OF3D_I32 = 5,
+    OF3D_F32 = 6,
+    OF3D_F64 = 7
+};
+
+/* arithmetic mode.  FP64_EXACT: fp64, no FMA contraction, scipy summation
+ * order — vx/vy/vz bit-identical to the reference.  OR in OF3D_REL_F64 to get
+ * the 3D reliability as float64 (the fp64 eigen-solve before the float32
+ * cast; MATLAB's calc_flow3D.m:235-236 keeps rel in double). */
+enum of3d_mode { OF3D_FP64_EXACT = 0, OF3D_REL_F64 = 0x100 };
+
+/* Filter taps (calc_flow.py:230-267).  Each vector has 2r+1 entries. */
+typedef struct of3d_taps {
+    const double* gauss;  /* fderiv == fx, radius rd = ceil(3*sig)       (:233,:253) */
+    const double* deriv;  /* fderiv*gderiv, radius rd, antisymmetric     (:239)      */
+    int rd;
+    const double* smooth; /* fsmooth, radius rs = ceil(3*sig/4)          (:234)      */
+    int rs;
+    const double* tderiv; /* ft*gt, radius rt = ceil(3*tSig), antisym.    (:260)      */
+    int rt;
+    const double* window; /* gw, radius rw = ceil(3*wSig)                (:264)      */
+    int rw;
+} of3d_taps;
+
+/* Optional timing record filled by the host entry points (milliseconds). */
+typedef struct of3d_perf {
+    double ms_h2d;     /* input upload                       */
+    double ms_kernels; /* device time of the kernel pipeline  */
+    double ms_d2h;     /* output download                     */
+    double ms_total;   /* wall time of the call               */
+} of3d_perf;
+
+typedef struct of3d_plan of3d_plan;
+
+/* Library version (OF3D_VERSION). */
+int of3d_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* of3d_last_error(void);
+
+/* Number of visible HIP devices (0 when no GPU / no driver). */
+int of3d_device_count(void);
+
+/* ---- host entry points (replace calc_flow3D / calc_flow2D) -------------- */
+
+/* calc_flow3D (calc_flow.py:175-360).  images: (nt, nz, ny, nx) of `dtype`;
+ * nt odd, only the centre frame c = (nt-1)/2 and frames c-rt..c+rt are read.
+ * vx, vy, vz: float64 (nz, ny, nx); rel: float32 (nz, ny, nx) — the reference
+ * returns rel from complex64 LAPACK, hence float32 (calc_flow.py:355-357) —
+ * or float64 when mode has OF3D_REL_F64. */
+int of3d_flow3d(const void* images, int dtype, int64_t nt, int64_t nz, int64_t ny, int64_t nx,
+                const of3d_taps* taps, int mode, int device, double* vx, double* vy, double* vz,
+                void* rel, of3d_perf* perf);
+
+/* calc_flow2D (calc_flow.py:18-173).  images (nt, ny, nx); outputs float64
+ * (ny, nx); rel = min root of the 2x2 characteristic quadratic (NaN where the
+ * discriminant rounds negative, as NumPy gives). */
+int of3d_flow2d(const void* images, int dtype, int64_t nt, int64_t ny, int64_t nx,
+                const of3d_taps* taps, int mode, int device, double* vx, double* vy, double* rel,
+                of3d_perf* perf);
+
+/* ---- device-resident plan (streaming driver, benchmarks, z-slab shards) -- */
+
+/* ndim 3: volume (nz, ny, nx); ndim 2: nz must be 1.  Allocates the device
+ * workspace on `device` for outputs over up to `max_out_planes` planes
+ * (<= 0: all nz). */
+int of3d_plan_create(of3d_plan** plan, int ndim, int64_t nz, int64_t ny, int64_t nx,
+                     const of3d_taps* taps, int mode, int device, int64_t max_out_planes);
+int of3d_plan_destroy(of3d_plan* plan);
+
+/* Device bytes held by the plan's workspace. */
+size_t of3d_plan_workspace_bytes(const of3d_plan* plan);
+
+/* Input planes a shard computing output planes [z_out0, z_out1) must hold
+ * resident (global plane indices [*z_in0, *z_in1)): the stencil halo. */
+int of3d_plan_input_range(const of3d_plan* plan, int64_t z_out0, int64_t z_out1, int64_t* z_in0,
+                          int64_t* z_in1);
+
+/* Run the pipeline for output planes [z_out0, z_out1) of the centre frame.
+ * d_frames: host array of 2*rt+1 DEVICE pointers, frame c-rt .. c+rt of the
+ *   stack, each pointing at global plane `frame_z0` of its frame (planes
+ *   contiguous, row stride nx, plane stride ny*nx, elements of `dtype`).
+ *   The frames must hold the planes of of3d_plan_input_range().
+ * d_vx/d_vy/d_vz: float64 (z_out1-z_out0, ny, nx) (d_vz ignored for 2D);
+ * d_rel: float32 for 3D (float64 if the plan's mode has OF3D_REL_F64),
+ * float64 for 2D.  stream: hipStream_t or NULL. */
+int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, int64_t frame_z0,
+                      int64_t z_out0, int64_t z_out1, double* d_vx, double* d_vy, double* d_vz,
+                      void* d_rel, void* stream);
+
+/* Per-stage timing with HIP events recorded on the launch stream.
+ * of3d_plan_set_timing(plan, slots): keep a ring of `slots` executions
+ * (0 = off; no host synchronisation is added to of3d_plan_execute).
+ * of3d_plan_stage_times: average device time (ms) per stage over the
+ * executions recorded since the previous read (at most `slots`), then reset;
+ * returns the number of stages written (<= cap).  Stage names:
+ * of3d_stage_name(i) = grad_xy, grad_z, prod_wy, wx, wz_solve. */
+int of3d_plan_set_timing(of3d_plan* plan, int slots);
+int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
+const char* of3d_stage_name(int i);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OF3D_H */

@@ -1,0 +1,182 @@
+"""ctypes binding of libof3d.so (include/of3d.h).
+
+The shared library is built in-tree (``opticalflow3d_dev_amd/libof3d.so``,
+``make -C opticalflow3d_dev_amd/csrc``).  There is no CPU fallback: if the
+library is missing or no GPU is visible, calls raise loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OF3D_LIB", os.path.join(_HERE, "libof3d.so"))
+
+OF3D_U8, OF3D_U16, OF3D_I16, OF3D_U32, OF3D_I32, OF3D_F32, OF3D_F64 = 1, 2, 3, 4, 5, 6, 7
+OF3D_FP64_EXACT = 0
+OF3D_REL_F64 = 0x100
+
+DTYPE_CODES = {
+    np.dtype(np.uint8): OF3D_U8,
+    np.dtype(np.uint16): OF3D_U16,
+    np.dtype(np.int16): OF3D_I16,
+    np.dtype(np.uint32): OF3D_U32,
+    np.dtype(np.int32): OF3D_I32,
+    np.dtype(np.float32): OF3D_F32,
+    np.dtype(np.float64): OF3D_F64,
+}
+
+# Every symbol include/of3d.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "of3d_version", "of3d_last_error", "of3d_device_count", "of3d_flow3d", "of3d_flow2d",
+    "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
+    "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
+)
+
+
+class Taps(ctypes.Structure):
+    _fields_ = [
+        ("gauss", ctypes.POINTER(ctypes.c_double)),
+        ("deriv", ctypes.POINTER(ctypes.c_double)),
+        ("rd", ctypes.c_int),
+        ("smooth", ctypes.POINTER(ctypes.c_double)),
+        ("rs", ctypes.c_int),
+        ("tderiv", ctypes.POINTER(ctypes.c_double)),
+        ("rt", ctypes.c_int),
+        ("window", ctypes.POINTER(ctypes.c_double)),
+        ("rw", ctypes.c_int),
+    ]
+
+
+class Perf(ctypes.Structure):
+    _fields_ = [("ms_h2d", ctypes.c_double), ("ms_kernels", ctypes.c_double),
+                ("ms_d2h", ctypes.c_double), ("ms_total", ctypes.c_double)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libof3d.so once; raise if it is absent (no silent fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"opticalflow3d_dev_amd: HIP library not built ({LIB_PATH} missing); "
+                "run `make -C opticalflow3d_dev_amd/csrc` or __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        D = ctypes.POINTER(ctypes.c_double)
+        F = ctypes.POINTER(ctypes.c_float)
+        i64 = ctypes.c_int64
+        lib.of3d_version.restype = ctypes.c_int
+        lib.of3d_last_error.restype = ctypes.c_char_p
+        lib.of3d_device_count.restype = ctypes.c_int
+        lib.of3d_flow3d.argtypes = [P, ctypes.c_int, i64, i64, i64, i64, ctypes.POINTER(Taps), ctypes.c_int,
+                                    ctypes.c_int, D, D, D, P, ctypes.POINTER(Perf)]
+        lib.of3d_flow3d.restype = ctypes.c_int
+        lib.of3d_flow2d.argtypes = [P, ctypes.c_int, i64, i64, i64, ctypes.POINTER(Taps), ctypes.c_int,
+                                    ctypes.c_int, D, D, D, ctypes.POINTER(Perf)]
+        lib.of3d_flow2d.restype = ctypes.c_int
+        lib.of3d_plan_create.argtypes = [ctypes.POINTER(P), ctypes.c_int, i64, i64, i64, ctypes.POINTER(Taps),
+                                         ctypes.c_int, ctypes.c_int, i64]
+        lib.of3d_plan_create.restype = ctypes.c_int
+        lib.of3d_plan_destroy.argtypes = [P]
+        lib.of3d_plan_destroy.restype = ctypes.c_int
+        lib.of3d_plan_workspace_bytes.argtypes = [P]
+        lib.of3d_plan_workspace_bytes.restype = ctypes.c_size_t
+        lib.of3d_plan_input_range.argtypes = [P, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        lib.of3d_plan_input_range.restype = ctypes.c_int
+        lib.of3d_plan_execute.argtypes = [P, ctypes.POINTER(P), ctypes.c_int, i64, i64, i64, P, P, P, P, P]
+        lib.of3d_plan_execute.restype = ctypes.c_int
+        lib.of3d_plan_stage_times.argtypes = [P, D, ctypes.c_int]
+        lib.of3d_plan_stage_times.restype = ctypes.c_int
+        lib.of3d_stage_name.argtypes = [ctypes.c_int]
+        lib.of3d_stage_name.restype = ctypes.c_char_p
+        lib.of3d_plan_set_timing.argtypes = [P, ctypes.c_int]
+        lib.of3d_plan_set_timing.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return load().of3d_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise RuntimeError("of3d: " + last_error())
+    return rc
+
+
+def device_index() -> int:
+    """GPU used by the host entry points: $OF3D_DEVICE, else $LOCAL_RANK, else 0."""
+    for k in ("OF3D_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(k)
+        if v is not None and v != "":
+            return int(v)
+    return 0
+
+
+class TapSet:
+    """Keeps the tap arrays alive and exposes the of3d_taps struct."""
+
+    def __init__(self, taps: dict):
+        self.arrays = {k: np.ascontiguousarray(v, dtype=np.float64) for k, v in taps.items()}
+        r = lambda k: len(self.arrays[k]) // 2
+        ptr = lambda k: self.arrays[k].ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        self.struct = Taps(ptr("gauss"), ptr("deriv"), r("gauss"), ptr("smooth"), r("smooth"),
+                           ptr("tderiv"), r("tderiv"), ptr("window"), r("window"))
+        self.rd, self.rs, self.rt, self.rw = r("gauss"), r("smooth"), r("tderiv"), r("window")
+
+
+class Plan:
+    """Device-resident plan (of3d_plan_*): inputs/outputs are device pointers."""
+
+    def __init__(self, ndim, nz, ny, nx, taps: dict, device=0, max_out_planes=0, timing=0, mode=0):
+        self.lib = load()
+        self.taps = TapSet(taps)
+        self.ndim, self.nz, self.ny, self.nx, self.device = ndim, nz, ny, nx, device
+        h = ctypes.c_void_p()
+        check(self.lib.of3d_plan_create(ctypes.byref(h), ndim, nz, ny, nx, ctypes.byref(self.taps.struct),
+                                        mode, device, max_out_planes))
+        self.handle = h
+        if timing:
+            check(self.lib.of3d_plan_set_timing(h, int(timing)))
+
+    @property
+    def workspace_bytes(self):
+        return self.lib.of3d_plan_workspace_bytes(self.handle)
+
+    def input_range(self, z_out0, z_out1):
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        check(self.lib.of3d_plan_input_range(self.handle, z_out0, z_out1, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def execute(self, frame_ptrs, dtype_code, frame_z0, z_out0, z_out1, vx, vy, vz, rel, stream=0):
+        arr = (ctypes.c_void_p * len(frame_ptrs))(*frame_ptrs)
+        check(self.lib.of3d_plan_execute(self.handle, arr, dtype_code, frame_z0, z_out0, z_out1,
+                                         vx, vy, vz, rel, stream or None))
+
+    def stage_times(self):
+        buf = (ctypes.c_double * 8)()
+        n = check(self.lib.of3d_plan_stage_times(self.handle, buf, 8))
+        return {self.lib.of3d_stage_name(i).decode(): buf[i] for i in range(n)}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.of3d_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

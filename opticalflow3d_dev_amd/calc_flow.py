@@ -1,0 +1,249 @@
+"""Host API mirroring the reference module ``calc_flow`` (src/Python/calc_flow.py).
+
+Same names, signatures, defaults, argument checks (``SystemExit`` with the
+reference's messages), output dtypes and output files; the arithmetic runs on
+the MI355X through ``libof3d.so`` (HIP kernels behind a C-ABI, include/of3d.h).
+
+* ``calc_flow3D(images, xyzSig=3, tSig=1, wSig=4) -> (vx, vy, vz, rel)``
+  — calc_flow.py:175-360.  vx/vy/vz float64, rel float32 (the reference's
+  rel comes from complex64 LAPACK, calc_flow.py:355-357).
+* ``calc_flow2D(images, xySig=3, tSig=1, wSig=4) -> (vx, vy, rel)``
+  — calc_flow.py:18-173, all float64.
+* ``process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3,
+  xyzSig=3, tSig=1, wSig=4)`` — calc_flow.py:362-625 (alias ``calc_flow``).
+
+There is no CPU fallback: without the HIP library or a GPU the calls raise.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import re
+import sys
+from datetime import datetime
+from pathlib import Path
+
+import numpy as np
+
+from . import _lib
+from . import tiff as tf
+from .taps import make_taps
+
+MSG_NDIM_3D = "ERROR: Input image must be a 3D matrix with dimensions N_T, N_Z, N_Y, N_X"
+MSG_NDIM_2D = "ERROR: Input image must be a 3D matrix with dimensions N_T, N_Y, N_X"
+MSG_EDGE = "ERROR: Input images will lead to edge effects. N_T must be >= 6*tSig+1"
+MSG_ODD = ("ERROR: Input images must have an odd number of timepoints. "
+           "Only the central time point is analyzed")
+
+_D = ctypes.POINTER(ctypes.c_double)
+_F = ctypes.POINTER(ctypes.c_float)
+
+last_perf = {}
+
+
+def _check_args(images, ndim, tSig, msg_ndim):
+    """T9: the reference's checks in its order (calc_flow.py:212-222 / :54-64)."""
+    if not (len(images.shape) == ndim):
+        sys.exit(msg_ndim)
+    Nt = images.shape[0]
+    if Nt < 6 * tSig + 1:
+        sys.exit(MSG_EDGE)
+    if not (Nt % 2):
+        sys.exit(MSG_ODD)
+
+
+def _device_array(images):
+    """C-contiguous native-endian array of a dtype the kernels read directly.
+
+    Other real dtypes are cast with astype(np.float64) — the same cast the
+    reference applies to every input (calc_flow.py:225 / :67)."""
+    a = np.asarray(images)
+    dt = a.dtype.newbyteorder("=") if a.dtype.byteorder not in ("=", "|") else a.dtype
+    if dt in _lib.DTYPE_CODES:
+        a = np.ascontiguousarray(a, dtype=dt)
+    else:
+        a = np.ascontiguousarray(a.astype(np.float64))
+    return a, _lib.DTYPE_CODES[a.dtype]
+
+
+def _perf_dict(perf):
+    return {"ms_h2d": perf.ms_h2d, "ms_kernels": perf.ms_kernels, "ms_d2h": perf.ms_d2h,
+            "ms_total": perf.ms_total}
+
+
+def calc_flow3D(images, xyzSig=3, tSig=1, wSig=4):
+    """Three-dimensional LK optical flow of the centre frame of ``images``.
+
+    images: (N_T, N_Z, N_Y, N_X), N_T odd and >= 6*tSig+1 (calc_flow.py:190-199).
+    Returns vx, vy, vz (float64, pixels/frame) and rel (float32, smallest
+    eigenvalue of A'wA)."""
+    return _flow3d(images, xyzSig, tSig, wSig, rel_fp64=False)
+
+
+def _flow3d(images, xyzSig, tSig, wSig, rel_fp64=False):
+    """calc_flow3D; rel_fp64=True returns the fp64 eigenvalue (MATLAB-style rel)."""
+    _check_args(images, 4, tSig, MSG_NDIM_3D)
+    taps = _lib.TapSet(make_taps(xyzSig, tSig, wSig))
+    a, code = _device_array(images)
+    Nt, Nz, Ny, Nx = a.shape
+    vx = np.empty((Nz, Ny, Nx), np.float64)
+    vy = np.empty_like(vx)
+    vz = np.empty_like(vx)
+    rel = np.empty((Nz, Ny, Nx), np.float64 if rel_fp64 else np.float32)
+    if vx.size == 0:
+        return vx, vy, vz, rel
+    lib = _lib.load()
+    perf = _lib.Perf()
+    _lib.check(lib.of3d_flow3d(a.ctypes.data, code, Nt, Nz, Ny, Nx, ctypes.byref(taps.struct),
+                               _lib.OF3D_FP64_EXACT | (_lib.OF3D_REL_F64 if rel_fp64 else 0), _lib.device_index(),
+                               vx.ctypes.data_as(_D), vy.ctypes.data_as(_D), vz.ctypes.data_as(_D), rel.ctypes.data,
+                               ctypes.byref(perf)))
+    last_perf.clear()
+    last_perf.update(_perf_dict(perf))
+    return vx, vy, vz, rel
+
+
+def calc_flow2D(images, xySig=3, tSig=1, wSig=4):
+    """Two-dimensional LK optical flow of the centre frame of ``images``.
+
+    images: (N_T, N_Y, N_X) (calc_flow.py:33-35).  Returns vx, vy, rel, all
+    float64; rel is NaN where the discriminant rounds negative (as NumPy)."""
+    _check_args(images, 3, tSig, MSG_NDIM_2D)
+    taps = _lib.TapSet(make_taps(xySig, tSig, wSig))
+    a, code = _device_array(images)
+    Nt, Ny, Nx = a.shape
+    vx = np.empty((Ny, Nx), np.float64)
+    vy = np.empty_like(vx)
+    rel = np.empty_like(vx)
+    if vx.size == 0:
+        return vx, vy, rel
+    lib = _lib.load()
+    perf = _lib.Perf()
+    _lib.check(lib.of3d_flow2d(a.ctypes.data, code, Nt, Ny, Nx, ctypes.byref(taps.struct),
+                               _lib.OF3D_FP64_EXACT, _lib.device_index(), vx.ctypes.data_as(_D),
+                               vy.ctypes.data_as(_D), rel.ctypes.data_as(_D), ctypes.byref(perf)))
+    last_perf.clear()
+    last_perf.update(_perf_dict(perf))
+    return vx, vy, rel
+
+
+def _now():
+    return str(datetime.now())
+
+
+def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSig=3, tSig=1, wSig=4):
+    """Parse a TIFF time lapse, run the flow per output frame, write TIFFs.
+
+    Mirrors calc_flow.py:362-625: same checks and messages, the same
+    ``OpticalFlow3D/<imNameSave>/`` (or ``OpticalFlow2D``) output folder,
+    ``<imNameSave>_parameters.csv`` and ``<imNameSave>_{vx,vy,[vz,]rel}_t%04d.tiff``
+    files, the same stdout lines.  Returns None."""
+    ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
+    imDir = Path(imDir)
+    if not imDir.is_dir():
+        sys.exit('ERROR: image path \'%s\' does not exist' % imDir)
+    imNamePattern = re.compile(imName + '.tif')
+    fileList = [f for f in os.listdir(imDir) if imNamePattern.fullmatch(f)]
+    if len(fileList) == 0:
+        sys.exit('ERROR: No image files found. imName: ' + imName + ' imDir: ' + str(imDir))
+    if fileType == 'OneTif':
+        if len(fileList) > 1:
+            sys.exit('ERROR: Type is OneTif but more than one file was found for imName: ' + imName)
+    elif fileType == 'SequenceT':
+        if len(fileList) < 6 * tSig + 1:
+            sys.exit('ERROR: Image sequence found for file name ' + imName + ' only contains '
+                     + str(len(fileList)) + ' files. Minimum 6*tsig+1 (' + str(6 * tSig + 1) + ') files required.')
+    else:
+        sys.exit('ERROR: fileType must be either OneTif or SequenceT.')
+    fileList = tf.natsorted(fileList)
+    if spatialDimensions < 2 or spatialDimensions > 3:
+        sys.exit('ERROR: Number of spatial dimensions must be either 2 or 3.')
+
+    ### Metadata parsing and parameter saving (calc_flow.py:445-494)
+    meta = tf.TiffFile(imDir / fileList[0])
+    Ny = meta.pages[0].shape[0]
+    Nx = meta.pages[0].shape[1]
+    imj = meta.imagej_metadata
+    if fileType == 'OneTif':
+        if not imj:
+            sys.exit('ERROR: fileType is OneTif, but no ImageJ metadata was detected')
+        Nt = imj["frames"]
+        if spatialDimensions == 3:
+            Nz = imj["slices"]
+        elif spatialDimensions == 2:
+            Nz = 1
+    elif fileType == 'SequenceT':
+        Nz = len(meta.pages)
+        Nt = len(fileList)
+        if spatialDimensions == 2:
+            if Nz != 1:
+                sys.exit('ERROR: More than one z-slice detected for 2D processing')
+        elif spatialDimensions == 3:
+            if Nz <= 1:
+                sys.exit('ERROR: 3D processing requested but Nz = ' + str(Nz))
+
+    NtChunk = 6 * tSig + 1
+    if not (NtChunk % 2):
+        NtChunk = NtChunk + 1
+    NtSlice = math.ceil(NtChunk / 2) - 1
+
+    savedir = imDir / ('OpticalFlow3D' if spatialDimensions == 3 else 'OpticalFlow2D')
+    savedir.mkdir(exist_ok=True)
+    imNameSave = imName.replace('.*', '')
+    savedir = savedir / imNameSave
+    savedir.mkdir(exist_ok=True)
+    _write_parameters(savedir / (imNameSave + '_parameters.csv'), xyzSig, tSig, wSig, Nx, Ny, Nz, Nt)
+
+    ### Processing Loop (calc_flow.py:497-625)
+    print('Note: regardless of input filenames, the first image = frame 0.')
+    print('If your file names start from 0, adjust indexing accordingly for reading the output files.')
+    print(' ')
+    for hh in range(0, NtSlice):
+        print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
+
+    prefix = str(savedir / imNameSave)
+    names = ('vx', 'vy', 'vz', 'rel') if spatialDimensions == 3 else ('vx', 'vy', 'rel')
+    flow = calc_flow3D if spatialDimensions == 3 else calc_flow2D
+
+    if fileType == 'OneTif':
+        allImages = tf.memmap(imDir / (imName + '.tif'))
+        load = lambda hh: allImages[hh:hh + NtChunk]
+    else:
+        load = lambda hh: np.stack([tf.imread(imDir / fileList[hh + jj]) for jj in range(NtChunk)])
+    for hh in range(0, int(Nt) - NtChunk + 1):
+        loopStart = datetime.now()
+        print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
+        images = load(hh)
+        out = flow(images, xyzSig, tSig, wSig)
+        tstr = str(hh + NtSlice).zfill(4)
+        for n, arr in zip(names, out):
+            tf.imwrite(prefix + '_' + n + '_t' + tstr + '.tiff', arr, photometric='minisblack')
+        del out, images
+        framestime = datetime.now()
+        print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(framestime - loopStart))
+
+    for hh in range(int(Nt) - NtSlice, int(Nt)):
+        print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
+
+
+calc_flow = process_flow
+
+
+def _fmt_csv(v):
+    if isinstance(v, (bool, np.bool_)):
+        return str(bool(v))
+    if isinstance(v, (int, np.integer)):
+        return str(int(v))
+    return repr(float(v))
+
+
+def _write_parameters(path, xyzSig, tSig, wSig, Nx, Ny, Nz, Nt):
+    """<imNameSave>_parameters.csv as pandas.DataFrame.to_csv(index=False) writes it
+    (calc_flow.py:485-494; column name 'tiSig' sic)."""
+    cols = ['xyzSig', 'tiSig', 'wSig', 'Nx', 'Ny', 'Nz', 'Nt']
+    vals = [xyzSig, tSig, wSig, Nx, Ny, Nz, Nt]
+    with open(path, 'w', newline='') as f:
+        f.write(','.join(cols) + '\n')
+        f.write(','.join(_fmt_csv(v) for v in vals) + '\n')

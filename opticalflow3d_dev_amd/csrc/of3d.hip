@@ -1,0 +1,897 @@
+// of3d.hip — MI355X (gfx950) Lucas–Kanade optical flow, fp64 exact mode.
+//
+// Re-design (not a port) of the hot path of ScientistRachel/OpticalFlow3D_dev
+// src/Python/calc_flow.py:175-360 (calc_flow3D) and :18-173 (calc_flow2D).
+// The reference runs 40 scipy.ndimage.correlate1d passes over full fp64
+// volumes plus a per-voxel LAPACK cgeev; here the same arithmetic is a
+// five-kernel device pipeline over HBM-resident fields:
+//
+//   K1 grad_xy  : temporal derivative of the centre frame (T2) + y and x passes
+//                 of the four gradient filters (T4), LDS-tiled, clamped halos
+//   K2 grad_z   : z pass of the four gradients (T4), register-blocked along z
+//   K3 prod_wy  : the 9 (2D: 5) structure-tensor products + W y pass (T5)
+//   K4 wx       : W x pass (T5), LDS row tiles
+//   K5 wz_solve : W z pass (T5) + closed-form 3x3 solve (T6) + fp64 smallest
+//                 eigenvalue (T7);  2D: closed-form 2x2 solve + rel (T8)
+//
+// Bit-exactness: every 1-D pass evaluates scipy's NI_Correlate1D order for
+// (anti)symmetric taps  o = c0*w0; for k=r..1: o += (c[-k] +- c[+k]) * w[-k]
+// with indices clamped to the GLOBAL volume edge at every pass
+// (mode='nearest'); products and the solve copy calc_flow.py's expression
+// trees.  Built with -ffp-contract=off (no FMA) and IEEE div/sqrt.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/of3d.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+    g_err = msg;
+    return -1;
+}
+
+#define OF3D_HIP(call)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) return fail(std::string(#call) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kMaxR = 64;          // largest supported tap radius
+constexpr int kMaxT = 2 * 32 + 1;  // largest temporal window (rt <= 32)
+constexpr double kEps = 2.220446049250313e-16;  // np.finfo(float).eps, calc_flow.py:155,338
+
+// Half taps on the device: h[0] = centre tap w[r], h[k] = w[r-k] (left side),
+// exactly the coefficients scipy multiplies by in the symmetric branch.
+struct DevTaps {
+    const double* g;  // gauss   (rd)
+    const double* d;  // deriv   (rd, antisymmetric)
+    const double* s;  // smooth  (rs)
+    const double* t;  // tderiv  (rt, antisymmetric)
+    const double* w;  // window  (rw)
+    int rd, rs, rt, rw;
+};
+
+struct Frames {
+    const void* p[kMaxT];  // frames c-rt .. c+rt
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+template <typename T>
+__device__ __forceinline__ double ldf(const void* p, size_t i) {
+    return (double)(reinterpret_cast<const T*>(p)[i]);
+}
+
+// One 1-D correlation along a strided axis, R consecutive outputs per thread
+// (register blocking: 2 loads per tap pair for all R outputs).  ld(i) returns
+// the value at (already clamped) axis index i.
+template <int R, bool ANTI, typename Load>
+__device__ __forceinline__ void pass_line(Load ld, int p0, int L, const double* __restrict__ h, int r,
+                                          double (&out)[R]) {
+    const int last = L - 1;
+#pragma unroll
+    for (int i = 0; i < R; ++i) out[i] = ld(clampi(p0 + i, 0, last)) * h[0];
+    double lo[R], hi[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        lo[i] = ld(clampi(p0 + i - r, 0, last));
+        hi[i] = ld(clampi(p0 + i + r, 0, last));
+    }
+    for (int k = r; k >= 1; --k) {
+        const double wk = h[k];
+#pragma unroll
+        for (int i = 0; i < R; ++i) out[i] = out[i] + (ANTI ? (lo[i] - hi[i]) : (lo[i] + hi[i])) * wk;
+        if (k > 1) {
+#pragma unroll
+            for (int i = 0; i < R - 1; ++i) lo[i] = lo[i + 1];
+            lo[R - 1] = ld(clampi(p0 + R - k, 0, last));
+#pragma unroll
+            for (int i = R - 1; i > 0; --i) hi[i] = hi[i - 1];
+            hi[0] = ld(clampi(p0 + k - 1, 0, last));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: temporal derivative + y/x passes of the gradient filters.
+//   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]       (calc_flow.py:279-288, y first)
+//   B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (dz)
+// Tile: K1_TX x-outputs x ty rows of one plane; LDS holds I and dt0 over the
+// (ty+2rd) x (K1_TX+2rd) clamped halo and the three y-pass results.
+// ---------------------------------------------------------------------------
+constexpr int K1_TX = 64;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_grad_xy(Frames fr, int ty, int ny, int nx, int frames_z0, int zb0,
+                                                 DevTaps tp, double* __restrict__ B, size_t fs, int need_b4) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int rd = tp.rd, rs = tp.rs, rt = tp.rt;
+    const int PW = K1_TX + 2 * rd;
+    const int RH = ty + 2 * rd;
+    double* sI = smem;
+    double* sT = sI + RH * PW;
+    double* sA1 = sT + RH * PW;
+    double* sA2 = sA1 + ty * PW;
+    double* sA3 = sA2 + ty * PW;
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * K1_TX, y0 = blockIdx.y * ty;
+    const int zl = blockIdx.z;
+    const size_t plane = (size_t)(zb0 + zl - frames_z0) * (size_t)ny * nx;
+
+    for (int e = tid; e < RH * PW; e += 256) {
+        const int row = e / PW, col = e - row * PW;
+        const int gy = clampi(y0 - rd + row, 0, ny - 1), gx = clampi(x0 - rd + col, 0, nx - 1);
+        const size_t idx = plane + (size_t)gy * nx + gx;
+        const double c = ldf<T>(fr.p[rt], idx);
+        double dt = c * tp.t[0];
+        for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * tp.t[k];
+        sI[e] = c;
+        sT[e] = dt;
+    }
+    __syncthreads();
+    for (int e = tid; e < ty * PW; e += 256) {
+        const int row = e / PW, col = e - row * PW;
+        const int c = (row + rd) * PW + col;
+        double a1 = sT[c] * tp.g[0], a2 = sI[c] * tp.d[0], a3 = sI[c] * tp.s[0];
+        for (int k = rd; k >= 1; --k) {
+            a1 = a1 + (sT[c - k * PW] + sT[c + k * PW]) * tp.g[k];
+            a2 = a2 + (sI[c - k * PW] - sI[c + k * PW]) * tp.d[k];
+        }
+        for (int k = rs; k >= 1; --k) a3 = a3 + (sI[c - k * PW] + sI[c + k * PW]) * tp.s[k];
+        sA1[e] = a1;
+        sA2[e] = a2;
+        sA3[e] = a3;
+    }
+    __syncthreads();
+    for (int e = tid; e < ty * K1_TX; e += 256) {
+        const int row = e / K1_TX, col = e - row * K1_TX;
+        const int gy = y0 + row, gx = x0 + col;
+        if (gy >= ny || gx >= nx) continue;
+        const int c = row * PW + col + rd;
+        double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
+        for (int k = rd; k >= 1; --k) {
+            b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
+            b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
+        }
+        for (int k = rs; k >= 1; --k) {
+            b2 = b2 + (sA2[c - k] + sA2[c + k]) * tp.s[k];
+            b4 = b4 + (sA3[c - k] + sA3[c + k]) * tp.s[k];
+        }
+        const size_t o = ((size_t)zl * ny + gy) * nx + gx;
+        B[o] = b1;
+        B[fs + o] = b2;
+        B[2 * fs + o] = b3;
+        if (need_b4) B[3 * fs + o] = b4;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: z pass of the gradients (calc_flow.py:279-288, last pass, axis 0):
+//   dt = z(G)[B1], dy = z(S)[B2], dx = z(S)[B3], dz = z(D)[B4]
+// ---------------------------------------------------------------------------
+constexpr int K2_R = 4;
+
+__global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, int zb0, double* __restrict__ G,
+                                                int zg0, int nzg, int nz, int ny, int nx, size_t fs, DevTaps tp) {
+    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= nx || y >= ny) return;
+    const int zl0 = blockIdx.z * K2_R;
+    const int p0 = zg0 + zl0;
+    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + x;
+    const double* b0 = B + col;
+    double out[K2_R];
+    auto store = [&](int f) {
+#pragma unroll
+        for (int i = 0; i < K2_R; ++i)
+            if (zl0 + i < nzg) G[f * fs + (size_t)(zl0 + i) * ps + col] = out[i];
+    };
+    {
+        const double* b = b0;
+        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.g, tp.rd, out);
+        store(0);
+    }
+    {
+        const double* b = b0 + fs;
+        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.s, tp.rs, out);
+        store(1);
+    }
+    {
+        const double* b = b0 + 2 * fs;
+        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.s, tp.rs, out);
+        store(2);
+    }
+    {
+        const double* b = b0 + 3 * fs;
+        pass_line<K2_R, true>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.d, tp.rd, out);
+        store(3);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3: structure-tensor products + W y pass (calc_flow.py:300-313; 2D :133-141).
+// Gradient field index: 0 dt, 1 dy, 2 dx, 3 dz.
+// 3D product order: tx ty tz xy xz x2 yz y2 z2 ;  2D: tx ty xy x2 y2.
+// ---------------------------------------------------------------------------
+constexpr int K3_R = 4;
+
+template <int NP>
+struct ProdTable;
+template <>
+struct ProdTable<9> {
+    static constexpr int a[9] = {2, 1, 3, 2, 2, 2, 1, 1, 3};
+    static constexpr int b[9] = {0, 0, 0, 1, 3, 2, 3, 1, 3};
+};
+template <>
+struct ProdTable<5> {
+    static constexpr int a[5] = {2, 1, 2, 2, 1};
+    static constexpr int b[5] = {0, 0, 1, 2, 1};
+};
+
+template <int NP>
+__global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
+                                                 int nx, size_t fs, const double* __restrict__ hw, int rw) {
+    const int x = blockIdx.x * 64 + threadIdx.x;
+    if (x >= nx) return;
+    const int y0 = (blockIdx.y * 4 + threadIdx.y) * K3_R;
+    if (y0 >= ny) return;
+    const int zl = blockIdx.z;
+    const size_t base = (size_t)zl * ny * nx + x;
+    double out[K3_R];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const double* ga = G + ProdTable<NP>::a[p] * fs + base;
+        const double* gb = G + ProdTable<NP>::b[p] * fs + base;
+        pass_line<K3_R, false>([&](int yy) { return ga[(size_t)yy * nx] * gb[(size_t)yy * nx]; }, y0, ny, hw, rw,
+                               out);
+        double* o = P + p * fs + base;
+#pragma unroll
+        for (int i = 0; i < K3_R; ++i)
+            if (y0 + i < ny) o[(size_t)(y0 + i) * nx] = out[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4: W x pass over NF fields, one LDS row segment per field.
+// ---------------------------------------------------------------------------
+constexpr int K4_TX = 256;
+
+template <int NF>
+__global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
+                                            size_t fs, const double* __restrict__ hw, int rw) {
+    extern __shared__ __attribute__((aligned(16))) double srow[];
+    const int PW = K4_TX + 2 * rw;
+    const int x0 = blockIdx.x * K4_TX, y = blockIdx.y, zl = blockIdx.z;
+    const size_t row = ((size_t)zl * ny + y) * nx;
+    for (int f = 0; f < NF; ++f)
+        for (int e = threadIdx.x; e < PW; e += 256) srow[f * PW + e] = P[f * fs + row + clampi(x0 - rw + e, 0, nx - 1)];
+    __syncthreads();
+    const int x = x0 + threadIdx.x;
+    if (x >= nx) return;
+    const int c = threadIdx.x + rw;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const double* s = srow + f * PW;
+        double o = s[c] * hw[0];
+        for (int k = rw; k >= 1; --k) o = o + (s[c - k] + s[c + k]) * hw[k];
+        Q[f * fs + row + x] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Solves.  Expression trees copied from calc_flow.py:337-340 (3D) and
+// :154-168 (2D); numpy's x**-1 is a correctly rounded reciprocal, x**2 = x*x.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void solve3(double x2, double y2, double z2, double xy, double xz, double yz, double tx,
+                                       double ty, double tz, double& vx, double& vy, double& vz) {
+    double det = x2 * y2 * z2;
+    det = det + 2.0 * xy * xz * yz;
+    det = det - y2 * (xz * xz);
+    det = det - z2 * (xy * xy);
+    det = det - x2 * (yz * yz);
+    const double nR = -(1.0 / (det + kEps));
+    vx = nR * ((y2 * z2 - yz * yz) * tx + (xz * yz - xy * z2) * ty + (xy * yz - xz * y2) * tz);
+    vy = nR * ((yz * xz - xy * z2) * tx + (x2 * z2 - xz * xz) * ty + (xz * xy - x2 * yz) * tz);
+    vz = nR * ((xy * yz - y2 * xz) * tx + (xy * xz - x2 * yz) * ty + (x2 * y2 - xy * xy) * tz);
+}
+
+// Smallest eigenvalue of the symmetric 3x3 [[a d e][d b f][e f c]] in fp64
+// (trigonometric closed form).  The reference gets it from LAPACK cgeev in
+// complex64 (calc_flow.py:355-357); fp64 here, stored as float32 like the
+// reference's output.
+__device__ __forceinline__ double eigmin3(double a, double b, double c, double d, double e, double f) {
+    const double p1 = d * d + e * e + f * f;
+    if (p1 == 0.0) return fmin(a, fmin(b, c));
+    const double q = (a + b + c) / 3.0;
+    const double aq = a - q, bq = b - q, cq = c - q;
+    const double p2 = aq * aq + bq * bq + cq * cq + 2.0 * p1;
+    const double p = sqrt(p2 / 6.0);
+    const double ip = 1.0 / p;
+    const double B11 = aq * ip, B22 = bq * ip, B33 = cq * ip, B12 = d * ip, B13 = e * ip, B23 = f * ip;
+    const double detB =
+        B11 * (B22 * B33 - B23 * B23) - B12 * (B12 * B33 - B23 * B13) + B13 * (B12 * B23 - B22 * B13);
+    double r = 0.5 * detB;
+    r = fmin(1.0, fmax(-1.0, r));
+    const double phi = acos(r) / 3.0;
+    return q + 2.0 * p * cos(phi + 2.0943951023931957);  // + 2*pi/3
+}
+
+constexpr int K5_R = 2;
+
+template <typename RelT>
+__global__ __launch_bounds__(256) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
+                                                  size_t fs, const double* __restrict__ hw, int rw, int zo0, int nzo,
+                                                  double* __restrict__ vx, double* __restrict__ vy,
+                                                  double* __restrict__ vz, RelT* __restrict__ rel) {
+    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= nx || y >= ny) return;
+    const int zl0 = blockIdx.z * K5_R;
+    const int p0 = zo0 + zl0;
+    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + x;
+    double acc[9][K5_R];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+        const double* q = Q + f * fs + col;
+        pass_line<K5_R, false>([&](int z) { return q[(size_t)(z - zq0) * ps]; }, p0, nz, hw, rw, acc[f]);
+    }
+#pragma unroll
+    for (int i = 0; i < K5_R; ++i) {
+        if (zl0 + i >= nzo) break;
+        // field order: tx ty tz xy xz x2 yz y2 z2
+        double ox, oy, oz;
+        solve3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i], acc[0][i], acc[1][i], acc[2][i], ox,
+               oy, oz);
+        const size_t o = (size_t)(zl0 + i) * ps + col;
+        vx[o] = ox;
+        vy[o] = oy;
+        vz[o] = oz;
+        rel[o] = (RelT)eigmin3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i]);
+    }
+}
+
+// 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
+__global__ __launch_bounds__(256) void k_solve2d(const double* __restrict__ Q, size_t fs, int n,
+                                                 double* __restrict__ vx, double* __restrict__ vy,
+                                                 double* __restrict__ rel) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double tx = Q[i], ty = Q[fs + i], xy = Q[2 * fs + i], x2 = Q[3 * fs + i], y2 = Q[4 * fs + i];
+    const double det = (x2 * y2) - (xy * xy);
+    const double R = 1.0 / (det + kEps);
+    vx[i] = R * ((y2 * -tx) + (-xy * -ty));
+    vy[i] = R * ((-xy * -tx) + (x2 * -ty));
+    const double tr = x2 + y2;
+    const double disc = tr * tr - 4.0 * det;
+    const double L1 = (tr + sqrt(disc)) / 2.0;
+    const double L2 = (tr - sqrt(disc)) / 2.0;
+    // np.minimum propagates NaN
+    rel[i] = (L1 != L1) ? L1 : ((L2 != L2) ? L2 : (L1 < L2 ? L1 : L2));
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+size_t dtype_size(int dt) {
+    switch (dt) {
+        case OF3D_U8: return 1;
+        case OF3D_U16:
+        case OF3D_I16: return 2;
+        case OF3D_U32:
+        case OF3D_I32:
+        case OF3D_F32: return 4;
+        case OF3D_F64: return 8;
+        default: return 0;
+    }
+}
+
+// scipy NI_Correlate1D symmetry classification: +1, -1, 0
+int symmetry(const double* w, int r) {
+    bool sym = true, anti = true;
+    for (int k = 1; k <= r; ++k) {
+        if (std::fabs(w[r + k] - w[r - k]) > kEps) sym = false;
+        if (std::fabs(w[r + k] + w[r - k]) > kEps) anti = false;
+    }
+    return sym ? 1 : (anti ? -1 : 0);
+}
+
+const char* kStageNames[] = {"grad_xy", "grad_z", "prod_wy", "wx", "wz_solve"};
+constexpr int kStages = 5;
+
+}  // namespace
+
+struct of3d_plan {
+    int ndim = 3;
+    bool rel64 = false;  // OF3D_REL_F64
+    int64_t nz = 1, ny = 1, nx = 1;
+    int rd = 0, rs = 0, rt = 0, rw = 0;
+    int device = 0;
+    int64_t cap_planes = 0;  // planes per workspace field
+    std::vector<double> htaps;  // host copy of half taps (g | d | s | t | w)
+    double* d_taps = nullptr;
+    double* X = nullptr;  // 9 fields
+    double* Y = nullptr;  // 9 fields
+    size_t fs = 0;        // field stride (elements)
+    hipStream_t stream = nullptr;
+    int k1_ty = 16;
+    size_t k1_lds = 0;
+    bool host_ev = false;            // host entry: record into ev[]
+    hipEvent_t ev[kStages + 1] = {};
+    int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
+    std::vector<hipEvent_t> tev;     // timing_slots * (kStages + 1)
+    int64_t tcount = 0;              // executions recorded since the last of3d_plan_stage_times
+    double stage_ms[kStages] = {};
+    int stages_run = 0;
+    // host-entry staging
+    void* d_in = nullptr;
+    size_t d_in_bytes = 0;
+    void* d_out = nullptr;
+    size_t d_out_bytes = 0;
+};
+
+namespace {
+
+int build_taps(const of3d_taps* t, of3d_plan* p) {
+    if (!t || !t->gauss || !t->deriv || !t->smooth || !t->tderiv || !t->window) return fail("of3d: null taps");
+    if (t->rd < 0 || t->rs < 0 || t->rt < 0 || t->rw < 0) return fail("of3d: negative tap radius");
+    if (t->rd > kMaxR || t->rs > kMaxR || t->rw > kMaxR) return fail("of3d: spatial tap radius exceeds 64");
+    if (2 * t->rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
+    struct {
+        const double* w;
+        int r;
+        int want;
+        const char* name;
+    } f[5] = {{t->gauss, t->rd, 1, "gauss"},
+              {t->deriv, t->rd, -1, "deriv"},
+              {t->smooth, t->rs, 1, "smooth"},
+              {t->tderiv, t->rt, -1, "tderiv"},
+              {t->window, t->rw, 1, "window"}};
+    p->htaps.clear();
+    for (auto& e : f) {
+        if (e.r > 0 && symmetry(e.w, e.r) != e.want)
+            return fail(std::string("of3d: taps '") + e.name + "' do not have the expected (anti)symmetry");
+        for (int k = 0; k <= e.r; ++k) p->htaps.push_back(e.w[e.r - k]);
+    }
+    p->rd = t->rd;
+    p->rs = t->rs;
+    p->rt = t->rt;
+    p->rw = t->rw;
+    return 0;
+}
+
+DevTaps dev_taps(const of3d_plan* p) {
+    DevTaps d;
+    const double* b = p->d_taps;
+    d.g = b;
+    d.d = d.g + p->rd + 1;
+    d.s = d.d + p->rd + 1;
+    d.t = d.s + p->rs + 1;
+    d.w = d.t + p->rt + 1;
+    d.rd = p->rd;
+    d.rs = p->rs;
+    d.rt = p->rt;
+    d.rw = p->rw;
+    return d;
+}
+
+unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+template <typename T>
+void launch_k1(dim3 g, size_t lds, hipStream_t s, const Frames& fr, int ty, int ny, int nx, int fz0, int zb0,
+               DevTaps tp, double* B, size_t fs, int need_b4) {
+    hipLaunchKernelGGL(k_grad_xy<T>, g, dim3(256), lds, s, fr, ty, ny, nx, fz0, zb0, tp, B, fs, need_b4);
+}
+
+int set_k1_attrs(of3d_plan* p) {
+    // pick the tallest tile whose LDS footprint fits
+    for (int ty : {16, 8, 4, 2, 1}) {
+        const size_t pw = K1_TX + 2 * p->rd, rh = ty + 2 * p->rd;
+        const size_t bytes = (2 * rh * pw + 3 * (size_t)ty * pw) * sizeof(double);
+        if (bytes <= 160 * 1024) {
+            p->k1_ty = ty;
+            p->k1_lds = bytes;
+            break;
+        }
+        if (ty == 1) return fail("of3d: xyzSig too large for the LDS tile");
+    }
+    const void* ks[] = {(const void*)k_grad_xy<uint8_t>,  (const void*)k_grad_xy<uint16_t>,
+                        (const void*)k_grad_xy<int16_t>,  (const void*)k_grad_xy<uint32_t>,
+                        (const void*)k_grad_xy<int32_t>,  (const void*)k_grad_xy<float>,
+                        (const void*)k_grad_xy<double>};
+    for (auto k : ks) OF3D_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k1_lds));
+    const int wx_lds = (int)(9 * (K4_TX + 2 * p->rw) * sizeof(double));
+    OF3D_HIP(hipFuncSetAttribute((const void*)k_wx<9>, hipFuncAttributeMaxDynamicSharedMemorySize, wx_lds));
+    OF3D_HIP(hipFuncSetAttribute((const void*)k_wx<5>, hipFuncAttributeMaxDynamicSharedMemorySize, wx_lds));
+    return 0;
+}
+
+struct Ranges {
+    int64_t zo0, zo1, zg0, zg1, zb0, zb1;
+};
+
+Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
+    Ranges r;
+    r.zo0 = zo0;
+    r.zo1 = zo1;
+    if (p->ndim == 2) {
+        r.zg0 = r.zb0 = 0;
+        r.zg1 = r.zb1 = 1;
+        return r;
+    }
+    r.zg0 = std::max<int64_t>(zo0 - p->rw, 0);
+    r.zg1 = std::min<int64_t>(zo1 + p->rw, p->nz);
+    r.zb0 = std::max<int64_t>(r.zg0 - p->rd, 0);
+    r.zb1 = std::min<int64_t>(r.zg1 + p->rd, p->nz);
+    return r;
+}
+
+int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, double* vx,
+        double* vy, double* vz, void* rel, hipStream_t s) {
+    if (!p) return fail("of3d: null plan");
+    if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
+    const Ranges R = ranges(p, zo0, zo1);
+    if (R.zb1 - R.zb0 > p->cap_planes) return fail("of3d: output range exceeds the plan's workspace");
+    if (frame_z0 > R.zb0) return fail("of3d: frames do not hold the stencil halo planes");
+    if (dtype_size(dtype) == 0) return fail("of3d: unsupported dtype");
+    const int ny = (int)p->ny, nx = (int)p->nx, nz = (int)p->nz;
+    Frames fr{};
+    for (int i = 0; i < 2 * p->rt + 1; ++i) {
+        if (!d_frames[i]) return fail("of3d: null frame pointer");
+        fr.p[i] = d_frames[i];
+    }
+    const DevTaps tp = dev_taps(p);
+    const size_t fs = p->fs;
+    const int nb = (int)(R.zb1 - R.zb0), ng = (int)(R.zg1 - R.zg0), no = (int)(R.zo1 - R.zo0);
+    hipEvent_t* evs = p->host_ev ? p->ev
+                      : (p->timing_slots ? &p->tev[(size_t)(p->tcount % p->timing_slots) * (kStages + 1)] : nullptr);
+#define OF3D_MARK(i) \
+    do { \
+        if (evs) OF3D_HIP(hipEventRecord(evs[i], s)); \
+    } while (0)
+    OF3D_MARK(0);
+    // K1
+    {
+        dim3 g(cdiv(nx, K1_TX), cdiv(ny, p->k1_ty), nb);
+        const int fz0 = (int)frame_z0, zb0 = (int)R.zb0, need_b4 = p->ndim == 3;
+        switch (dtype) {
+            case OF3D_U8: launch_k1<uint8_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_U16: launch_k1<uint16_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_I16: launch_k1<int16_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_U32: launch_k1<uint32_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_I32: launch_k1<int32_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_F32: launch_k1<float>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_F64: launch_k1<double>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+        }
+        OF3D_HIP(hipGetLastError());
+    }
+    OF3D_MARK(1);
+    const double* G;
+    if (p->ndim == 3) {
+        dim3 g(cdiv(nx, 64), cdiv(ny, 4), cdiv(ng, K2_R));
+        hipLaunchKernelGGL(k_grad_z, g, dim3(64, 4), 0, s, p->X, (int)R.zb0, p->Y, (int)R.zg0, ng, nz, ny, nx, fs, tp);
+        OF3D_HIP(hipGetLastError());
+        G = p->Y;
+    } else {
+        G = p->X;
+    }
+    OF3D_MARK(2);
+    double* P = p->ndim == 3 ? p->X : p->Y;
+    double* Q = p->ndim == 3 ? p->Y : p->X;
+    {
+        dim3 g(cdiv(nx, 64), cdiv(ny, 4 * K3_R), ng);
+        if (p->ndim == 3)
+            hipLaunchKernelGGL(k_prod_wy<9>, g, dim3(64, 4), 0, s, G, P, ny, nx, fs, tp.w, tp.rw);
+        else
+            hipLaunchKernelGGL(k_prod_wy<5>, g, dim3(64, 4), 0, s, G, P, ny, nx, fs, tp.w, tp.rw);
+        OF3D_HIP(hipGetLastError());
+    }
+    OF3D_MARK(3);
+    {
+        dim3 g(cdiv(nx, K4_TX), ny, ng);
+        if (p->ndim == 3) {
+            const size_t lds = 9 * (K4_TX + 2 * p->rw) * sizeof(double);
+            hipLaunchKernelGGL(k_wx<9>, g, dim3(256), lds, s, P, Q, ny, nx, fs, tp.w, tp.rw);
+        } else {
+            const size_t lds = 5 * (K4_TX + 2 * p->rw) * sizeof(double);
+            hipLaunchKernelGGL(k_wx<5>, g, dim3(256), lds, s, P, Q, ny, nx, fs, tp.w, tp.rw);
+        }
+        OF3D_HIP(hipGetLastError());
+    }
+    OF3D_MARK(4);
+    if (p->ndim == 3) {
+        dim3 g(cdiv(nx, 64), cdiv(ny, 4), cdiv(no, K5_R));
+        if (p->rel64)
+            hipLaunchKernelGGL(k_wz_solve<double>, g, dim3(64, 4), 0, s, Q, (int)R.zg0, nz, ny, nx, fs, tp.w, tp.rw,
+                               (int)R.zo0, no, vx, vy, vz, (double*)rel);
+        else
+            hipLaunchKernelGGL(k_wz_solve<float>, g, dim3(64, 4), 0, s, Q, (int)R.zg0, nz, ny, nx, fs, tp.w, tp.rw,
+                               (int)R.zo0, no, vx, vy, vz, (float*)rel);
+    } else {
+        const int n = ny * nx;
+        hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);
+    }
+    OF3D_HIP(hipGetLastError());
+    OF3D_MARK(5);
+    p->stages_run = kStages;
+    if (!p->host_ev && p->timing_slots) ++p->tcount;
+#undef OF3D_MARK
+    return 0;
+}
+
+int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
+                int device, int64_t max_out_planes) {
+    if (!out) return fail("of3d: null plan pointer");
+    *out = nullptr;
+    if ((mode & ~OF3D_REL_F64) != OF3D_FP64_EXACT) return fail("of3d: unsupported mode");
+    if (ndim != 2 && ndim != 3) return fail("of3d: ndim must be 2 or 3");
+    if (ndim == 2 && nz != 1) return fail("of3d: 2D plans need nz == 1");
+    if (nz < 1 || ny < 1 || nx < 1) return fail("of3d: empty volume");
+    if (ny * nx > (int64_t)INT32_MAX || nz > 65535) return fail("of3d: volume too large for one plan");
+    std::unique_ptr<of3d_plan> p(new of3d_plan);
+    p->ndim = ndim;
+    p->rel64 = (mode & OF3D_REL_F64) != 0;
+    p->nz = nz;
+    p->ny = ny;
+    p->nx = nx;
+    p->device = device;
+    if (build_taps(taps, p.get())) return -1;
+    OF3D_HIP(hipSetDevice(device));
+    if (set_k1_attrs(p.get())) return -1;
+    int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
+    p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
+    p->fs = (size_t)p->cap_planes * ny * nx;
+    OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
+    OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
+    OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * sizeof(double)));
+    OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * sizeof(double)));
+    OF3D_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    for (auto& e : p->ev) OF3D_HIP(hipEventCreate(&e));
+    *out = p.release();
+    return 0;
+}
+
+void plan_free(of3d_plan* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
+    (void)hipFree(p->d_taps);
+    (void)hipFree(p->X);
+    (void)hipFree(p->Y);
+    (void)hipFree(p->d_in);
+    (void)hipFree(p->d_out);
+    for (auto& e : p->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : p->tev) (void)hipEventDestroy(e);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+// ---- host-entry plan cache (one plan per thread's last shape) ------------
+struct CacheKey {
+    int ndim, device, mode;
+    int64_t nz, ny, nx;
+    std::vector<double> taps;
+    std::vector<int> radii;
+    bool operator==(const CacheKey& o) const {
+        return ndim == o.ndim && device == o.device && mode == o.mode && nz == o.nz && ny == o.ny && nx == o.nx && taps == o.taps &&
+               radii == o.radii;
+    }
+};
+
+std::mutex g_cache_mu;
+struct CacheEntry {
+    CacheKey key;
+    of3d_plan* plan = nullptr;
+};
+std::vector<CacheEntry> g_cache;  // small LRU
+
+CacheKey make_key(int ndim, int device, int mode, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* t) {
+    CacheKey k{ndim, device, mode, nz, ny, nx, {}, {t->rd, t->rs, t->rt, t->rw}};
+    auto add = [&](const double* w, int r) { k.taps.insert(k.taps.end(), w, w + 2 * r + 1); };
+    add(t->gauss, t->rd);
+    add(t->deriv, t->rd);
+    add(t->smooth, t->rs);
+    add(t->tderiv, t->rt);
+    add(t->window, t->rw);
+    return k;
+}
+
+int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, int64_t ny, int64_t nx,
+              const of3d_taps* taps, int mode, int device, double* vx, double* vy, double* vz, void* rel,
+              of3d_perf* perf) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!images || !vx || !vy || !rel || (ndim == 3 && !vz)) return fail("of3d: null buffer");
+    if (!taps) return fail("of3d: null taps");
+    const size_t es = dtype_size(dtype);
+    if (!es) return fail("of3d: unsupported dtype");
+    if (nt < 1 || !(nt & 1)) return fail("of3d: nt must be odd");
+    const int64_t c = nt / 2;  // ceil(Nt/2)-1 for odd Nt (calc_flow.py:223)
+    const int rt = taps->rt;
+    if (taps->rt < 0 || 2 * rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    CacheKey key = make_key(ndim, device, mode, nz, ny, nx, taps);
+    of3d_plan* p = nullptr;
+    for (size_t i = 0; i < g_cache.size(); ++i)
+        if (g_cache[i].key == key) {
+            p = g_cache[i].plan;
+            std::rotate(g_cache.begin(), g_cache.begin() + i, g_cache.begin() + i + 1);
+            break;
+        }
+    if (!p) {
+        if (plan_create(&p, ndim, nz, ny, nx, taps, mode, device, 0)) return -1;
+        g_cache.insert(g_cache.begin(), CacheEntry{key, p});
+        while (g_cache.size() > 2) {
+            plan_free(g_cache.back().plan);
+            g_cache.pop_back();
+        }
+    }
+    OF3D_HIP(hipSetDevice(device));
+    const size_t vox = (size_t)nz * ny * nx;
+    // Only frames c-rt..c+rt enter the result (time indices clamped to [0,nt)).
+    const int nwin = 2 * rt + 1;
+    const size_t in_bytes = (size_t)nwin * vox * es;
+    if (p->d_in_bytes < in_bytes) {
+        (void)hipFree(p->d_in);
+        p->d_in = nullptr;
+        OF3D_HIP(hipMalloc(&p->d_in, in_bytes));
+        p->d_in_bytes = in_bytes;
+    }
+    const size_t rel_es = (ndim == 3 && !(mode & OF3D_REL_F64)) ? sizeof(float) : sizeof(double);
+    const size_t out_bytes = vox * (3 * sizeof(double) + rel_es);
+    if (p->d_out_bytes < out_bytes) {
+        (void)hipFree(p->d_out);
+        p->d_out = nullptr;
+        OF3D_HIP(hipMalloc(&p->d_out, out_bytes));
+        p->d_out_bytes = out_bytes;
+    }
+    hipStream_t s = p->stream;
+    hipEvent_t e0 = p->ev[0], e1 = p->ev[1];
+    const void* dptr[kMaxT];
+    // distinct frames needed, uploaded once each
+    std::vector<int64_t> src(nwin);
+    for (int i = 0; i < nwin; ++i) src[i] = std::min<int64_t>(std::max<int64_t>(c - rt + i, 0), nt - 1);
+    for (int i = 0; i < nwin; ++i) {
+        char* dst = (char*)p->d_in + (size_t)i * vox * es;
+        dptr[i] = dst;
+        OF3D_HIP(hipMemcpyAsync(dst, (const char*)images + (size_t)src[i] * vox * es, vox * es, hipMemcpyHostToDevice, s));
+    }
+    OF3D_HIP(hipStreamSynchronize(s));
+    const auto t1 = std::chrono::steady_clock::now();
+    double* dvx = (double*)p->d_out;
+    double* dvy = dvx + vox;
+    double* dvz = dvy + vox;
+    void* drel = (void*)(dvz + vox);
+    p->host_ev = true;
+    int rc = run(p, dptr, dtype, 0, 0, nz, dvx, dvy, ndim == 3 ? dvz : nullptr, drel, s);
+    p->host_ev = false;
+    if (rc) return rc;
+    OF3D_HIP(hipStreamSynchronize(s));
+    float kms = 0.f;
+    OF3D_HIP(hipEventElapsedTime(&kms, p->ev[0], p->ev[kStages]));
+    for (int i = 0; i < kStages; ++i) {
+        float m = 0.f;
+        (void)hipEventElapsedTime(&m, p->ev[i], p->ev[i + 1]);
+        p->stage_ms[i] = m;
+    }
+    (void)e0;
+    (void)e1;
+    const auto t2 = std::chrono::steady_clock::now();
+    OF3D_HIP(hipMemcpyAsync(vx, dvx, vox * sizeof(double), hipMemcpyDeviceToHost, s));
+    OF3D_HIP(hipMemcpyAsync(vy, dvy, vox * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (ndim == 3) OF3D_HIP(hipMemcpyAsync(vz, dvz, vox * sizeof(double), hipMemcpyDeviceToHost, s));
+    OF3D_HIP(hipMemcpyAsync(rel, drel, vox * rel_es, hipMemcpyDeviceToHost, s));
+    OF3D_HIP(hipStreamSynchronize(s));
+    const auto t3 = std::chrono::steady_clock::now();
+    if (perf) {
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        perf->ms_h2d = ms(t0, t1);
+        perf->ms_kernels = kms;
+        perf->ms_d2h = ms(t2, t3);
+        perf->ms_total = ms(t0, t3);
+    }
+    return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int of3d_version(void) { return OF3D_VERSION; }
+
+const char* of3d_last_error(void) { return g_err.c_str(); }
+
+int of3d_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int of3d_flow3d(const void* images, int dtype, int64_t nt, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps,
+                int mode, int device, double* vx, double* vy, double* vz, void* rel, of3d_perf* perf) {
+    return host_flow(3, images, dtype, nt, nz, ny, nx, taps, mode, device, vx, vy, vz, rel, perf);
+}
+
+int of3d_flow2d(const void* images, int dtype, int64_t nt, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
+                int device, double* vx, double* vy, double* rel, of3d_perf* perf) {
+    return host_flow(2, images, dtype, nt, 1, ny, nx, taps, mode, device, vx, vy, nullptr, rel, perf);
+}
+
+int of3d_plan_create(of3d_plan** plan, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
+                     int device, int64_t max_out_planes) {
+    return plan_create(plan, ndim, nz, ny, nx, taps, mode, device, max_out_planes);
+}
+
+int of3d_plan_destroy(of3d_plan* plan) {
+    plan_free(plan);
+    return 0;
+}
+
+size_t of3d_plan_workspace_bytes(const of3d_plan* p) { return p ? 18 * p->fs * sizeof(double) : 0; }
+
+int of3d_plan_input_range(const of3d_plan* p, int64_t zo0, int64_t zo1, int64_t* zi0, int64_t* zi1) {
+    if (!p || !zi0 || !zi1) return fail("of3d: null argument");
+    if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
+    const Ranges r = ranges(p, zo0, zo1);
+    *zi0 = r.zb0;
+    *zi1 = r.zb1;
+    return 0;
+}
+
+int of3d_plan_execute(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1,
+                      double* vx, double* vy, double* vz, void* rel, void* stream) {
+    if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
+    OF3D_HIP(hipSetDevice(p->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
+}
+
+int of3d_plan_set_timing(of3d_plan* p, int slots) {
+    if (!p) return fail("of3d: null plan");
+    if (slots < 0 || slots > 4096) return fail("of3d: timing slots must be in [0, 4096]");
+    OF3D_HIP(hipSetDevice(p->device));
+    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
+    for (auto e : p->tev) (void)hipEventDestroy(e);
+    p->tev.assign((size_t)slots * (kStages + 1), nullptr);
+    for (auto& e : p->tev) OF3D_HIP(hipEventCreate(&e));
+    p->timing_slots = slots;
+    p->tcount = 0;
+    return 0;
+}
+
+int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
+    if (!p || !ms) return fail("of3d: null argument");
+    if (!p->timing_slots) return fail("of3d: timing not enabled on this plan");
+    const int64_t n = std::min<int64_t>(p->tcount, p->timing_slots);
+    if (n == 0) return fail("of3d: no timed executions since the last read");
+    const int m = std::min(cap, kStages);
+    std::vector<double> acc(kStages, 0.0);
+    for (int64_t j = 0; j < n; ++j) {
+        hipEvent_t* e = &p->tev[(size_t)j * (kStages + 1)];
+        OF3D_HIP(hipEventSynchronize(e[kStages]));
+        for (int i = 0; i < kStages; ++i) {
+            float t = 0.f;
+            OF3D_HIP(hipEventElapsedTime(&t, e[i], e[i + 1]));
+            acc[i] += t;
+        }
+    }
+    for (int i = 0; i < m; ++i) ms[i] = acc[i] / (double)n;
+    p->tcount = 0;
+    return m;
+}
+
+const char* of3d_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
+
+}  // extern "C"

@@ -1,0 +1,374 @@
+"""Minimal TIFF reader/writer for the process_flow driver.
+
+The reference driver uses ``tifffile`` (calc_flow.py:12) for four things:
+``TiffFile(...).pages[0].shape`` / ``len(pages)`` / ``imagej_metadata``
+(calc_flow.py:445-465), ``memmap`` of an ImageJ hyperstack (:509),
+``imread`` of one file per time point (:571-574) and
+``imwrite(path, arr, photometric='minisblack')`` for the outputs (:526-529).
+``tifffile`` is not installed in this image, so this module implements that
+subset from the TIFF 6.0 / BigTIFF layout:
+
+* reading: classic and BigTIFF, either byte order, uncompressed strips,
+  uint8/16/32, int8/16/32, float32/64 samples, one sample per pixel; ImageJ
+  hyperstacks whose image data is one contiguous block (ImageJ writes > 4 GB
+  stacks with a single IFD and contiguous planes — the case the MATLAB twin
+  handles in ``M/TIFFvolume.m:48-52,82-115``);
+* writing: little-endian, uncompressed, one page per leading-axis slice with a
+  tifffile-style shaped JSON description on the first page and
+  SampleFormat/BitsPerSample from the array dtype; BigTIFF automatically once
+  the file would pass ~4 GB (tifffile's threshold).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import re
+import struct
+
+import numpy as np
+
+_TYPES = {1: ("B", 1), 2: ("s", 1), 3: ("H", 2), 4: ("I", 4), 5: ("II", 8), 6: ("b", 1), 7: ("B", 1),
+          8: ("h", 2), 9: ("i", 4), 10: ("ii", 8), 11: ("f", 4), 12: ("d", 8), 16: ("Q", 8), 17: ("q", 8),
+          18: ("Q", 8)}
+
+
+class Page:
+    def __init__(self, tags, bo):
+        self.tags = tags
+        self.byteorder = bo
+        self.width = int(tags[256][0])
+        self.length = int(tags[257][0])
+        bps = tags.get(258, (1,))
+        self.bits = int(bps[0])
+        self.spp = int(tags.get(277, (1,))[0])
+        self.compression = int(tags.get(259, (1,))[0])
+        fmt = int(tags.get(339, (1,))[0])
+        kind = {1: "u", 2: "i", 3: "f"}.get(fmt)
+        if kind is None:
+            raise ValueError(f"unsupported SampleFormat {fmt}")
+        self.dtype = np.dtype(f"{bo}{kind}{self.bits // 8}")
+        self.offsets = [int(v) for v in tags.get(273, ())]
+        self.counts = [int(v) for v in tags.get(279, ())]
+        desc = tags.get(270)
+        self.description = desc if isinstance(desc, str) else None
+
+    @property
+    def shape(self):
+        if self.spp > 1:
+            return (self.length, self.width, self.spp)
+        return (self.length, self.width)
+
+    @property
+    def nbytes(self):
+        return self.length * self.width * self.spp * self.dtype.itemsize
+
+    def contiguous_offset(self):
+        """Offset of the page data if its strips are one contiguous block."""
+        if self.compression != 1 or not self.offsets:
+            return None
+        pos = self.offsets[0]
+        for o, c in zip(self.offsets, self.counts):
+            if o != pos:
+                return None
+            pos += c
+        return self.offsets[0]
+
+
+def _parse_imagej(desc):
+    if not desc or not desc.startswith("ImageJ="):
+        return None
+    out = {}
+    for line in desc.splitlines():
+        if "=" not in line:
+            continue
+        k, v = line.split("=", 1)
+        v = v.strip()
+        for conv in (int, float):
+            try:
+                v = conv(v)
+                break
+            except ValueError:
+                pass
+        else:
+            if v in ("true", "false"):
+                v = v == "true"
+        out[k.strip()] = v
+    return out
+
+
+class TiffFile:
+    """Subset of tifffile.TiffFile: ``pages``, ``imagej_metadata``, ``asarray``, ``memmap``."""
+
+    def __init__(self, path):
+        self.path = os.fspath(path)
+        with open(self.path, "rb") as f:
+            head = f.read(16)
+            if head[:2] == b"II":
+                bo = "<"
+            elif head[:2] == b"MM":
+                bo = ">"
+            else:
+                raise ValueError(f"{self.path}: not a TIFF file")
+            magic = struct.unpack(bo + "H", head[2:4])[0]
+            if magic == 42:
+                self.bigtiff = False
+                first = struct.unpack(bo + "I", head[4:8])[0]
+            elif magic == 43:
+                self.bigtiff = True
+                first = struct.unpack(bo + "Q", head[8:16])[0]
+            else:
+                raise ValueError(f"{self.path}: bad TIFF magic {magic}")
+            self.byteorder = bo
+            self.pages = []
+            seen = set()
+            off = first
+            while off and off not in seen:
+                seen.add(off)
+                tags, off = self._read_ifd(f, off)
+                self.pages.append(Page(tags, bo))
+        self.imagej_metadata = _parse_imagej(self.pages[0].description) if self.pages else None
+        self.shaped_metadata = None
+        d = self.pages[0].description if self.pages else None
+        if d and d.startswith("{"):
+            try:
+                self.shaped_metadata = json.loads(d)
+            except ValueError:
+                pass
+
+    def _read_ifd(self, f, off):
+        bo = self.byteorder
+        f.seek(off)
+        if self.bigtiff:
+            n = struct.unpack(bo + "Q", f.read(8))[0]
+            esz, vsz = 20, 8
+        else:
+            n = struct.unpack(bo + "H", f.read(2))[0]
+            esz, vsz = 12, 4
+        raw = f.read(n * esz)
+        nxt_raw = f.read(vsz)
+        nxt = struct.unpack(bo + ("Q" if self.bigtiff else "I"), nxt_raw)[0] if len(nxt_raw) == vsz else 0
+        tags = {}
+        for i in range(n):
+            e = raw[i * esz:(i + 1) * esz]
+            if self.bigtiff:
+                code, typ, cnt = struct.unpack(bo + "HHQ", e[:12])
+                val = e[12:20]
+            else:
+                code, typ, cnt = struct.unpack(bo + "HHI", e[:8])
+                val = e[8:12]
+            if typ not in _TYPES:
+                continue
+            fmt, size = _TYPES[typ]
+            total = size * cnt
+            if total > vsz:
+                ptr = struct.unpack(bo + ("Q" if self.bigtiff else "I"), val)[0]
+                pos = f.tell()
+                f.seek(ptr)
+                data = f.read(total)
+                f.seek(pos)
+            else:
+                data = val[:total]
+            if typ == 2:
+                tags[code] = data.rstrip(b"\0").decode("latin-1")
+            elif typ in (5, 10):
+                tags[code] = struct.unpack(bo + fmt[0] * (2 * cnt), data)
+            else:
+                tags[code] = struct.unpack(bo + fmt * cnt, data)
+        return tags, nxt
+
+    # -- series shape (tifffile's "series[0]" for the layouts handled here)
+    def series_shape(self):
+        p0 = self.pages[0]
+        ij = self.imagej_metadata
+        if ij:
+            images = int(ij.get("images", len(self.pages)))
+            dims = []
+            for k in ("frames", "slices", "channels"):
+                v = int(ij.get(k, 1))
+                if v > 1:
+                    dims.append(v)
+            shape = tuple(dims) + p0.shape
+            if int(np.prod(dims or [1])) != images:
+                shape = ((images,) if images > 1 else ()) + p0.shape
+            return shape
+        if self.shaped_metadata and "shape" in self.shaped_metadata:
+            return tuple(int(v) for v in self.shaped_metadata["shape"])
+        if len(self.pages) == 1:
+            return p0.shape
+        return (len(self.pages),) + p0.shape
+
+    def _contiguous_block(self):
+        """(offset, count) if all series images form one contiguous block."""
+        p0 = self.pages[0]
+        shape = self.series_shape()
+        nimg = int(np.prod(shape)) // int(np.prod(p0.shape))
+        off0 = p0.contiguous_offset()
+        if off0 is None:
+            return None
+        if len(self.pages) >= nimg:
+            pos = off0
+            for p in self.pages[:nimg]:
+                if p.contiguous_offset() != pos or p.shape != p0.shape or p.dtype != p0.dtype:
+                    return None
+                pos += p.nbytes
+        elif not self.imagej_metadata:
+            return None  # ImageJ >4 GB stacks: one IFD, planes contiguous after it
+        return off0, nimg
+
+    def memmap(self):
+        blk = self._contiguous_block()
+        if blk is None:
+            raise ValueError(f"{self.path}: image data is not contiguous; cannot memory-map")
+        return np.memmap(self.path, dtype=self.pages[0].dtype, mode="r", offset=blk[0], shape=self.series_shape())
+
+    def asarray(self):
+        blk = self._contiguous_block()
+        shape = self.series_shape()
+        p0 = self.pages[0]
+        if blk is not None:
+            with open(self.path, "rb") as f:
+                f.seek(blk[0])
+                buf = f.read(int(np.prod(shape)) * p0.dtype.itemsize)
+            return np.frombuffer(buf, dtype=p0.dtype).reshape(shape).astype(p0.dtype.newbyteorder("="))
+        out = []
+        with open(self.path, "rb") as f:
+            for p in self.pages:
+                if p.compression != 1:
+                    raise ValueError(f"{self.path}: compressed TIFF (compression={p.compression}) not supported")
+                chunks = []
+                for o, c in zip(p.offsets, p.counts):
+                    f.seek(o)
+                    chunks.append(f.read(c))
+                out.append(np.frombuffer(b"".join(chunks), dtype=p.dtype)[: int(np.prod(p.shape))].reshape(p.shape))
+        arr = np.stack(out) if len(out) > 1 else out[0]
+        return arr.reshape(shape).astype(p0.dtype.newbyteorder("="))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def imread(path):
+    return TiffFile(path).asarray()
+
+
+def memmap(path):
+    return TiffFile(path).memmap()
+
+
+_BIGTIFF_THRESHOLD = 2**32 - 2**25  # tifffile switches to BigTIFF past this size
+
+
+def imwrite(path, data, photometric="minisblack", description=None, imagej=False, bigtiff=None):
+    """Write ``data`` as an uncompressed little-endian TIFF, one page per 2-D plane.
+
+    Layout (as tifffile lays out one series): header, first IFD with the
+    description, then the image data of all pages as ONE contiguous block (so
+    the file can be memory-mapped), then the IFDs of the remaining pages."""
+    if photometric not in ("minisblack", None):
+        raise ValueError("only photometric='minisblack' is supported")
+    arr = np.asarray(data)
+    if arr.dtype.kind == "b":
+        arr = arr.astype(np.uint8)
+    arr = np.ascontiguousarray(arr, dtype=arr.dtype.newbyteorder("<"))
+    if arr.ndim < 2:
+        arr = arr.reshape((1,) * (2 - arr.ndim) + arr.shape)
+    ny, nx = arr.shape[-2:]
+    npages = int(np.prod(arr.shape[:-2])) if arr.ndim > 2 else 1
+    fmt = {"u": 1, "i": 2, "f": 3}[arr.dtype.kind]
+    bits = arr.dtype.itemsize * 8
+    if description is None:
+        description = imagej_description(arr.shape) if imagej else json.dumps({"shape": list(arr.shape)})
+    desc = description.encode("latin-1") + b"\0"
+    software = b"opticalflow3d_dev_amd\0"
+    plane_bytes = ny * nx * arr.dtype.itemsize
+    if bigtiff is None:
+        bigtiff = npages * (plane_bytes + 320) + len(desc) + 64 > _BIGTIFF_THRESHOLD
+    ofmt, osz = ("Q", 8) if bigtiff else ("I", 4)
+    cfmt, csz = ("Q", 8) if bigtiff else ("H", 2)
+    esz = 20 if bigtiff else 12
+    otyp = 16 if bigtiff else 4
+
+    def entry(code, typ, count, value_bytes):
+        head = struct.pack("<HHQ", code, typ, count) if bigtiff else struct.pack("<HHI", code, typ, count)
+        return head + value_bytes.ljust(osz, b"\0")
+
+    def ifd_block(i, pos, data_pos):
+        """IFD of page i at byte `pos` (+ its out-of-line values); next-IFD field left 0."""
+        ntags = 13 if i == 0 else 12
+        extra_pos = pos + csz + ntags * esz + osz
+        extras = b""
+        desc_pos = extra_pos
+        if i == 0:
+            extras += desc + (b"\0" if len(desc) & 1 else b"")
+        soft_pos = extra_pos + len(extras)
+        extras += software + (b"\0" if len(software) & 1 else b"")
+        u32 = lambda v: struct.pack("<I", v)
+        u16 = lambda v: struct.pack("<H", v)
+        off = lambda v: struct.pack("<" + ofmt, v)
+        tags = [entry(254, 4, 1, u32(0)), entry(256, 4, 1, u32(nx)), entry(257, 4, 1, u32(ny)),
+                entry(258, 3, 1, u16(bits)), entry(259, 3, 1, u16(1)), entry(262, 3, 1, u16(1))]
+        if i == 0:
+            tags.append(entry(270, 2, len(desc), off(desc_pos)))
+        tags += [entry(273, otyp, 1, off(data_pos)), entry(277, 3, 1, u16(1)), entry(278, 4, 1, u32(ny)),
+                 entry(279, otyp, 1, off(plane_bytes)), entry(305, 2, len(software), off(soft_pos)),
+                 entry(339, 3, 1, u16(fmt))]
+        assert len(tags) == ntags
+        body = struct.pack("<" + cfmt, ntags) + b"".join(tags)
+        return body, body + struct.pack("<" + ofmt, 0) + extras
+
+    header = b"II" + (struct.pack("<HHHQ", 43, 8, 0, 16) if bigtiff else struct.pack("<HI", 42, 8))
+    ifd0_pos = len(header)
+    # size of IFD0 block does not depend on data_pos; place data after it, 16-B aligned
+    _, blk0 = ifd_block(0, ifd0_pos, 0)
+    data_pos = ifd0_pos + len(blk0)
+    data_pos += (-data_pos) % 16
+    flat = arr.reshape(-1)
+    with open(path, "wb") as f:
+        f.write(header)
+        body0, blk0 = ifd_block(0, ifd0_pos, data_pos)
+        f.write(blk0)
+        f.write(b"\0" * (data_pos - f.tell()))
+        f.write(flat.tobytes())
+        prev_next = ifd0_pos + len(body0)
+        for i in range(1, npages):
+            pos = f.tell()
+            pos += pos & 1
+            f.write(b"\0" * (pos - f.tell()))
+            body, blk = ifd_block(i, pos, data_pos + i * plane_bytes)
+            f.write(blk)
+            end = f.tell()
+            f.seek(prev_next)
+            f.write(struct.pack("<" + ofmt, pos))
+            f.seek(end)
+            prev_next = pos + len(body)
+
+
+def imagej_description(shape, frames=None, slices=None):
+    """ImageJ hyperstack description for (T, Z, Y, X) / (T, Y, X) data."""
+    if frames is None:
+        if len(shape) == 4:
+            frames, slices = shape[0], shape[1]
+        elif len(shape) == 3:
+            frames, slices = shape[0], 1
+        else:
+            frames, slices = 1, 1
+    images = frames * slices
+    lines = ["ImageJ=1.11a", f"images={images}"]
+    if slices > 1:
+        lines.append(f"slices={slices}")
+    if frames > 1:
+        lines.append(f"frames={frames}")
+    lines += ["hyperstack=true", "mode=grayscale", "loop=false"]
+    return "\n".join(lines) + "\n"
+
+
+def natsorted(items):
+    """Natural sort (natsort.natsorted default: unsigned integers compared numerically)."""
+    def key(s):
+        parts = re.split(r"(\d+)", s)
+        return [(0, int(p)) if p.isdigit() else (1, p) for p in parts]
+    return sorted(items, key=key)

@@ -1,0 +1,131 @@
+"""Host-side logic (CPU only, no device calls): taps, argument checks, TIFF
+I/O, natural sort, parameters CSV, process_flow's file discovery errors."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, golden_cases, golden_manifest, load_golden
+from opticalflow3d_dev_amd import calc_flow2D, calc_flow3D, make_taps, process_flow, radii
+from opticalflow3d_dev_amd import tiff as tf
+from opticalflow3d_dev_amd.calc_flow import _write_parameters
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_product_taps_match_reference_bits(name):
+    g = load_golden(name)
+    t = make_taps(g["sig"], g["tsig"], g["wsig"])
+    for k, v in t.items():
+        assert bits_equal(v, g["taps"][k]), k
+    rd, rs, rt, rw = radii(g["sig"], g["tsig"], g["wsig"])
+    assert (len(t["gauss"]), len(t["smooth"]), len(t["tderiv"]), len(t["window"])) == \
+        (2 * rd + 1, 2 * rs + 1, 2 * rt + 1, 2 * rw + 1)
+
+
+def test_product_error_messages_match_reference():
+    """SystemExit text identical to the reference (checks run before any device call)."""
+    for name, e in golden_manifest()["_errors"].items():
+        fn = calc_flow3D if e["dims"] == 3 else calc_flow2D
+        with pytest.raises(SystemExit) as ex:
+            fn(np.zeros(e["shape"], np.uint16), 1, e["tSig"], 2)
+        assert str(ex.value.code) == e["message"], name
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int16, np.float32, np.float64])
+@pytest.mark.parametrize("shape", [(5, 7), (3, 4, 6), (2, 3, 4, 5)])
+def test_tiff_roundtrip(tmp_path, dtype, shape):
+    a = (np.random.default_rng(0).uniform(0, 100, size=shape)).astype(dtype)
+    p = tmp_path / "x.tiff"
+    tf.imwrite(p, a, photometric="minisblack")
+    b = tf.imread(p)
+    assert b.shape == a.shape and b.dtype == a.dtype and np.array_equal(a, b)
+    t = tf.TiffFile(p)
+    assert len(t.pages) == (int(np.prod(shape[:-2])) if len(shape) > 2 else 1)
+    assert t.pages[0].shape == shape[-2:]
+    m = tf.memmap(p)
+    assert np.array_equal(np.asarray(m), a)
+
+
+def test_tiff_bigtiff_roundtrip(tmp_path):
+    a = np.arange(2 * 3 * 4, dtype=np.float64).reshape(2, 3, 4)
+    p = tmp_path / "big.tiff"
+    tf.imwrite(p, a, bigtiff=True)
+    assert tf.TiffFile(p).bigtiff
+    assert np.array_equal(tf.imread(p), a)
+
+
+def test_tiff_float32_readable_by_pillow(tmp_path):
+    from PIL import Image
+    a = np.random.default_rng(1).normal(size=(3, 6, 5)).astype(np.float32)
+    p = tmp_path / "rel.tiff"
+    tf.imwrite(p, a)
+    im = Image.open(p)
+    for i in range(3):
+        im.seek(i)
+        assert np.array_equal(np.asarray(im, dtype=np.float32), a[i])
+
+
+def test_imagej_hyperstack_memmap(tmp_path):
+    a = np.random.default_rng(2).integers(0, 4000, size=(7, 3, 5, 6)).astype(np.uint16)
+    p = tmp_path / "stack.tif"
+    tf.imwrite(p, a, imagej=True)
+    t = tf.TiffFile(p)
+    ij = t.imagej_metadata
+    assert ij["frames"] == 7 and ij["slices"] == 3 and ij["images"] == 21
+    m = tf.memmap(p)
+    assert m.shape == (7, 3, 5, 6) and np.array_equal(np.asarray(m), a)
+
+
+def test_imagej_single_ifd_contiguous(tmp_path):
+    """ImageJ > 4 GB layout: one IFD, planes contiguous after it (M/TIFFvolume.m:48-52)."""
+    a = np.random.default_rng(3).integers(0, 4000, size=(7, 2, 4, 5)).astype(np.uint16)
+    p = tmp_path / "one_ifd.tif"
+    tf.imwrite(p, a[0, 0], description=tf.imagej_description(a.shape))
+    # append the remaining planes contiguously after the first page's data
+    t = tf.TiffFile(p)
+    off = t.pages[0].offsets[0]
+    with open(p, "r+b") as f:
+        f.seek(off)
+        f.write(a.tobytes())
+    assert np.array_equal(np.asarray(tf.memmap(p)), a)
+
+
+def test_natsorted():
+    names = ["im_t10.tif", "im_t2.tif", "im_t1.tif", "im_t100.tif", "im_t20.tif"]
+    assert tf.natsorted(names) == ["im_t1.tif", "im_t2.tif", "im_t10.tif", "im_t20.tif", "im_t100.tif"]
+
+
+def test_parameters_csv(tmp_path):
+    p = tmp_path / "x_parameters.csv"
+    _write_parameters(p, 3, 1, 4, 512, 256, 64, 13)
+    assert p.read_text() == "xyzSig,tiSig,wSig,Nx,Ny,Nz,Nt\n3,1,4,512,256,64,13\n"
+    _write_parameters(p, 1.5, 1, 2.5, 8, 8, 1, 7)
+    assert p.read_text() == "xyzSig,tiSig,wSig,Nx,Ny,Nz,Nt\n1.5,1,2.5,8,8,1,7\n"
+
+
+def test_process_flow_errors(tmp_path):
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path / "nope"), "x")
+    assert str(e.value.code) == "ERROR: image path '%s' does not exist" % (tmp_path / "nope")
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "x")
+    assert str(e.value.code) == "ERROR: No image files found. imName: x imDir: " + str(tmp_path)
+    for i in range(3):
+        tf.imwrite(tmp_path / f"s_t{i}.tif", np.zeros((4, 4), np.uint16))
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "s_t.*", "SequenceT", 2)
+    assert str(e.value.code) == ("ERROR: Image sequence found for file name s_t.* only contains 3 files. "
+                                 "Minimum 6*tsig+1 (7) files required.")
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "s_t.*", "OneTif", 2)
+    assert str(e.value.code) == "ERROR: Type is OneTif but more than one file was found for imName: s_t.*"
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "s_t.*", "Other", 2)
+    assert str(e.value.code) == "ERROR: fileType must be either OneTif or SequenceT."
+    tf.imwrite(tmp_path / "plain.tif", np.zeros((2, 4, 4), np.uint16))
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "plain", "OneTif", 3)
+    assert str(e.value.code) == "ERROR: fileType is OneTif, but no ImageJ metadata was detected"
+    with pytest.raises(SystemExit) as e:
+        process_flow(str(tmp_path), "plain", "OneTif", 4)
+    assert str(e.value.code) == "ERROR: Number of spatial dimensions must be either 2 or 3."
