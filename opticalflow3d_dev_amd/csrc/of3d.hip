@@ -29,6 +29,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/of3d.h"
@@ -48,7 +49,7 @@ int fail(const std::string& msg) {
         if (e_ != hipSuccess) return fail(std::string(#call) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-constexpr int kMaxR = 64;          // largest supported tap radius
+constexpr int kMaxR = 48;          // largest supported tap radius (LDS tiles)
 constexpr int kMaxT = 2 * 32 + 1;  // largest temporal window (rt <= 32)
 constexpr double kEps = 2.220446049250313e-16;  // np.finfo(float).eps, calc_flow.py:155,338
 
@@ -219,12 +220,62 @@ __global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, in
     }
 }
 
+// 1-D pass over a staged LDS line, R consecutive outputs per thread at line
+// positions base..base+R-1 (elements `st` doubles apart); the staged line
+// already holds the clamped halo (positions base-r .. base+R-1+r valid).
+// Summation order per output is scipy's: o = c*w0; k = r..1: o += (lo +- hi)*w.
+//
+// Register reuse without register moves: at step q (k = r-q) output i needs
+// lo = s[base-r+q+i] and hi = s[base+r-q+i].  Both are streams indexed by
+// (q+i) and (q-i); each lives in an R-slot ring (L[m % R], U[m % R]), and
+// the q loop is unrolled by R so every slot index is a compile-time constant.
+// Per step: 2 LDS reads, 3R fp64 ops, ~3R live doubles, any radius.
+template <int R, bool ANTI>
+__device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, int base,
+                                         const double* __restrict__ h, int r, double (&out)[R]) {
+    double L[R], U[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        out[i] = s[(base + i) * st] * h[0];
+        L[i] = s[(base - r + i) * st];                   // S_lo[i]
+        U[(R - i) % R] = s[(base + r + i) * st];        // S_hi[-i]  -> slot (-i mod R)
+    }
+    // one step q (k = r - q) with ring phase j = q mod R (compile-time)
+    auto step = [&](int q, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        const double wk = h[r - q];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const double lo = L[(i + j) % R];
+            const double hi = U[(j - i + R) % R];
+            out[i] = out[i] + (ANTI ? (lo - hi) : (lo + hi)) * wk;
+        }
+        // refill (always inside the staged window, also after the last step)
+        L[j] = s[(base - r + q + R) * st];           // S_lo[q+R]
+        U[(j + 1) % R] = s[(base + r - q - 1) * st];  // S_hi[q+1]
+    };
+    int q = 0;
+    for (; q + R <= r; q += R) {
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (step(q + J, std::integral_constant<int, J>{}), ...);
+        }(std::make_integer_sequence<int, R>{});
+    }
+    const int t = r - q;  // 0 .. R-1 remaining steps, phases 0 .. t-1
+    [&]<int... J>(std::integer_sequence<int, J...>) {
+        ((J < t ? step(q + J, std::integral_constant<int, J>{}) : void()), ...);
+    }(std::make_integer_sequence<int, R - 1>{});
+}
+
 // ---------------------------------------------------------------------------
 // K3: structure-tensor products + W y pass (calc_flow.py:300-313; 2D :133-141).
 // Gradient field index: 0 dt, 1 dy, 2 dx, 3 dz.
 // 3D product order: tx ty tz xy xz x2 yz y2 z2 ;  2D: tx ty xy x2 y2.
+// Block = 64 x-columns x K3_YC rows of one plane.  Per product: the product
+// over the (K3_YC + 2rw)-row clamped halo is staged in LDS (double-buffered;
+// the next product's gradient loads are in flight during this product's
+// pass), then each thread produces K3_R rows by a register-rotated window.
 // ---------------------------------------------------------------------------
-constexpr int K3_R = 4;
+constexpr int K3_R = 8, K3_YC = 4 * K3_R;
 
 template <int NP>
 struct ProdTable;
@@ -239,53 +290,95 @@ struct ProdTable<5> {
     static constexpr int b[5] = {0, 0, 1, 2, 1};
 };
 
-template <int NP>
-__global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
+template <int NP, int NJ>
+__global__ __launch_bounds__(256, 2) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
                                                  int nx, size_t fs, const double* __restrict__ hw, int rw) {
-    const int x = blockIdx.x * 64 + threadIdx.x;
-    if (x >= nx) return;
-    const int y0 = (blockIdx.y * 4 + threadIdx.y) * K3_R;
-    if (y0 >= ny) return;
-    const int zl = blockIdx.z;
-    const size_t base = (size_t)zl * ny * nx + x;
-    double out[K3_R];
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int H = K3_YC + 2 * rw;
+    const int lane = threadIdx.x, g = threadIdx.y;
+    const int x = blockIdx.x * 64 + lane;
+    const int xs = x < nx ? x : nx - 1;
+    const int y0 = blockIdx.y * K3_YC;
+    const size_t pl = (size_t)blockIdx.z * ny * nx;
+    double ra[NJ], rb[NJ];
+    // packed product table (4 bits per entry), runtime-indexed
+    constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // a[] = {2,1,3,2,2,2,1,1,3} / {2,1,2,2,1}
+    constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;  // b[] = {0,0,0,1,3,2,3,1,3} / {0,0,1,2,1}
+    auto fetch = [&](int p) {
+        const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
+        const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
 #pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int row = g + 4 * j;
+            if (row < H) {
+                const size_t o = (size_t)clampi(y0 - rw + row, 0, ny - 1) * nx;
+                ra[j] = ga[o];
+                rb[j] = gb[o];
+            }
+        }
+    };
+    fetch(0);
+#pragma unroll 1
     for (int p = 0; p < NP; ++p) {
-        const double* ga = G + ProdTable<NP>::a[p] * fs + base;
-        const double* gb = G + ProdTable<NP>::b[p] * fs + base;
-        pass_line<K3_R, false>([&](int yy) { return ga[(size_t)yy * nx] * gb[(size_t)yy * nx]; }, y0, ny, hw, rw,
-                               out);
-        double* o = P + p * fs + base;
+        double* buf = sm + (p & 1) * H * 64;
 #pragma unroll
-        for (int i = 0; i < K3_R; ++i)
-            if (y0 + i < ny) o[(size_t)(y0 + i) * nx] = out[i];
+        for (int j = 0; j < NJ; ++j) {
+            const int row = g + 4 * j;
+            if (row < H) buf[row * 64 + lane] = ra[j] * rb[j];
+        }
+        __syncthreads();
+        if (p + 1 < NP) fetch(p + 1);
+        double out[K3_R];
+        lds_pass<K3_R, false>(buf + lane, 64, rw + g * K3_R, hw, rw, out);
+        if (x < nx) {
+            double* o = P + p * fs + pl + x;
+#pragma unroll
+            for (int i = 0; i < K3_R; ++i) {
+                const int y = y0 + g * K3_R + i;
+                if (y < ny) o[(size_t)y * nx] = out[i];
+            }
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
-// K4: W x pass over NF fields, one LDS row segment per field.
+// K4: W x pass over NF fields.  Block = 64 rows x K4_TX x-outputs of one
+// plane; lane = row, so each thread walks its row with a register-rotated
+// window (K4_R outputs) over an LDS tile of odd pitch (conflict-free column
+// access); results go back through LDS for coalesced row stores.
 // ---------------------------------------------------------------------------
-constexpr int K4_TX = 256;
+constexpr int K4_R = 16, K4_TX = 4 * K4_R, K4_ROWS = 64;
 
 template <int NF>
-__global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
+__global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
                                             size_t fs, const double* __restrict__ hw, int rw) {
-    extern __shared__ __attribute__((aligned(16))) double srow[];
-    const int PW = K4_TX + 2 * rw;
-    const int x0 = blockIdx.x * K4_TX, y = blockIdx.y, zl = blockIdx.z;
-    const size_t row = ((size_t)zl * ny + y) * nx;
-    for (int f = 0; f < NF; ++f)
-        for (int e = threadIdx.x; e < PW; e += 256) srow[f * PW + e] = P[f * fs + row + clampi(x0 - rw + e, 0, nx - 1)];
-    __syncthreads();
-    const int x = x0 + threadIdx.x;
-    if (x >= nx) return;
-    const int c = threadIdx.x + rw;
-#pragma unroll
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int W = K4_TX + 2 * rw;
+    const int PP = W | 1;
+    const int lane = threadIdx.x, g = threadIdx.y;
+    const int x0 = blockIdx.x * K4_TX, y0 = blockIdx.y * K4_ROWS;
+    const size_t pl = (size_t)blockIdx.z * ny * nx;
+#pragma unroll 1
     for (int f = 0; f < NF; ++f) {
-        const double* s = srow + f * PW;
-        double o = s[c] * hw[0];
-        for (int k = rw; k >= 1; --k) o = o + (s[c - k] + s[c + k]) * hw[k];
-        Q[f * fs + row + x] = o;
+        const double* src = P + f * fs + pl;
+        for (int row = g; row < K4_ROWS; row += 4) {
+            const double* r = src + (size_t)min(y0 + row, ny - 1) * nx;
+            for (int c = lane; c < W; c += 64) sm[row * PP + c] = r[clampi(x0 - rw + c, 0, nx - 1)];
+        }
+        __syncthreads();
+        double out[K4_R];
+        lds_pass<K4_R, false>(sm + lane * PP, 1, rw + g * K4_R, hw, rw, out);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < K4_R; ++i) sm[lane * PP + g * K4_R + i] = out[i];
+        __syncthreads();
+        double* dst = Q + f * fs + pl;
+        const int x = x0 + lane;
+        for (int row = g; row < K4_ROWS; row += 4) {
+            const int y = y0 + row;
+            if (y < ny && x < nx) dst[(size_t)y * nx + x] = sm[row * PP + lane];
+        }
+        __syncthreads();
     }
 }
 
@@ -327,32 +420,59 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     return q + 2.0 * p * cos(phi + 2.0943951023931957);  // + 2*pi/3
 }
 
-constexpr int K5_R = 2;
+// K5: W z pass + solve + reliability.  Block = 64 x-columns of one row and
+// K5_ZC output planes; per field the (K5_ZC + 2rw)-plane clamped window is
+// staged in LDS (double-buffered, next field's loads in flight during this
+// field's pass); each thread keeps its K5_R outputs of all 9 fields in
+// registers for the pointwise solve.
+constexpr int K5_R = 4, K5_ZC = 4 * K5_R;
 
-template <typename RelT>
-__global__ __launch_bounds__(256) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
+template <typename RelT, int NJ>
+__global__ __launch_bounds__(256, 2) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
                                                   size_t fs, const double* __restrict__ hw, int rw, int zo0, int nzo,
                                                   double* __restrict__ vx, double* __restrict__ vy,
                                                   double* __restrict__ vz, RelT* __restrict__ rel) {
-    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
-    if (x >= nx || y >= ny) return;
-    const int zl0 = blockIdx.z * K5_R;
-    const int p0 = zo0 + zl0;
-    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + x;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int H = K5_ZC + 2 * rw;
+    const int lane = threadIdx.x, g = threadIdx.y;
+    const int x = blockIdx.x * 64 + lane;
+    const int xs = x < nx ? x : nx - 1;
+    const int y = blockIdx.y;
+    const int zc0 = zo0 + blockIdx.z * K5_ZC;
+    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + xs;
+    double rq[NJ];
+    auto fetch = [&](int f) {
+        const double* q = Q + f * fs + col;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int row = g + 4 * j;
+            if (row < H) rq[j] = q[(size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps];
+        }
+    };
     double acc[9][K5_R];
+    fetch(0);
 #pragma unroll
     for (int f = 0; f < 9; ++f) {
-        const double* q = Q + f * fs + col;
-        pass_line<K5_R, false>([&](int z) { return q[(size_t)(z - zq0) * ps]; }, p0, nz, hw, rw, acc[f]);
+        double* buf = sm + (f & 1) * H * 64;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int row = g + 4 * j;
+            if (row < H) buf[row * 64 + lane] = rq[j];
+        }
+        __syncthreads();
+        if (f + 1 < 9) fetch(f + 1);
+        lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
     }
+    if (x >= nx) return;
 #pragma unroll
     for (int i = 0; i < K5_R; ++i) {
-        if (zl0 + i >= nzo) break;
+        const int zl = zc0 + g * K5_R + i - zo0;
+        if (zl >= nzo) break;
         // field order: tx ty tz xy xz x2 yz y2 z2
         double ox, oy, oz;
         solve3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i], acc[0][i], acc[1][i], acc[2][i], ox,
                oy, oz);
-        const size_t o = (size_t)(zl0 + i) * ps + col;
+        const size_t o = (size_t)zl * ps + (size_t)y * nx + x;
         vx[o] = ox;
         vy[o] = oy;
         vz[o] = oz;
@@ -424,7 +544,7 @@ struct of3d_plan {
     size_t fs = 0;        // field stride (elements)
     hipStream_t stream = nullptr;
     int k1_ty = 16;
-    size_t k1_lds = 0;
+    size_t k1_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
@@ -444,7 +564,7 @@ namespace {
 int build_taps(const of3d_taps* t, of3d_plan* p) {
     if (!t || !t->gauss || !t->deriv || !t->smooth || !t->tderiv || !t->window) return fail("of3d: null taps");
     if (t->rd < 0 || t->rs < 0 || t->rt < 0 || t->rw < 0) return fail("of3d: negative tap radius");
-    if (t->rd > kMaxR || t->rs > kMaxR || t->rw > kMaxR) return fail("of3d: spatial tap radius exceeds 64");
+    if (t->rd > kMaxR || t->rs > kMaxR || t->rw > kMaxR) return fail("of3d: spatial tap radius exceeds 48");
     if (2 * t->rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
     struct {
         const double* w;
@@ -492,6 +612,33 @@ void launch_k1(dim3 g, size_t lds, hipStream_t s, const Frames& fr, int ty, int 
     hipLaunchKernelGGL(k_grad_xy<T>, g, dim3(256), lds, s, fr, ty, ny, nx, fz0, zb0, tp, B, fs, need_b4);
 }
 
+// W-pass kernel variants: rows of a staged window each thread prefetches
+// into registers (4 row-groups) — NJ >= ceil(H/4).
+int nj_for(int h) { return h <= 64 ? 16 : (h <= 80 ? 20 : (h <= 96 ? 24 : 32)); }
+
+template <int NJ3, int NJ5>
+struct WKernels {
+    static const void* k3_9() { return (const void*)k_prod_wy<9, NJ3>; }
+    static const void* k3_5() { return (const void*)k_prod_wy<5, NJ3>; }
+    static const void* k4_9() { return (const void*)k_wx<9>; }
+    static const void* k4_5() { return (const void*)k_wx<5>; }
+    static const void* k5_f() { return (const void*)k_wz_solve<float, NJ5>; }
+    static const void* k5_d() { return (const void*)k_wz_solve<double, NJ5>; }
+};
+
+template <typename F>
+void for_each_w_kernel(int rw, F&& f) {
+    auto call = [&](auto K) { f(K.k3_9(), K.k3_5(), K.k4_9(), K.k4_5(), K.k5_f(), K.k5_d()); };
+    const int nj3 = nj_for(K3_YC + 2 * rw), nj5 = nj_for(K5_ZC + 2 * rw);
+    if (nj3 == 16 && nj5 == 16) call(WKernels<16, 16>{});
+    else if (nj3 == 20 && nj5 == 16) call(WKernels<20, 16>{});
+    else if (nj3 == 24 && nj5 == 16) call(WKernels<24, 16>{});
+    else if (nj3 == 24 && nj5 == 20) call(WKernels<24, 20>{});
+    else if (nj3 == 24 && nj5 == 24) call(WKernels<24, 24>{});
+    else if (nj3 == 32 && nj5 == 24) call(WKernels<32, 24>{});
+    else call(WKernels<32, 32>{});
+}
+
 int set_k1_attrs(of3d_plan* p) {
     // pick the tallest tile whose LDS footprint fits
     for (int ty : {16, 8, 4, 2, 1}) {
@@ -509,11 +656,27 @@ int set_k1_attrs(of3d_plan* p) {
                         (const void*)k_grad_xy<int32_t>,  (const void*)k_grad_xy<float>,
                         (const void*)k_grad_xy<double>};
     for (auto k : ks) OF3D_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k1_lds));
-    const int wx_lds = (int)(9 * (K4_TX + 2 * p->rw) * sizeof(double));
-    OF3D_HIP(hipFuncSetAttribute((const void*)k_wx<9>, hipFuncAttributeMaxDynamicSharedMemorySize, wx_lds));
-    OF3D_HIP(hipFuncSetAttribute((const void*)k_wx<5>, hipFuncAttributeMaxDynamicSharedMemorySize, wx_lds));
-    return 0;
+    // W-pass tiles
+    p->k3_lds = (size_t)2 * (K3_YC + 2 * p->rw) * 64 * sizeof(double);
+    p->k4_lds = (size_t)K4_ROWS * ((K4_TX + 2 * p->rw) | 1) * sizeof(double);
+    p->k5_lds = (size_t)2 * (K5_ZC + 2 * p->rw) * 64 * sizeof(double);
+    const size_t lim = 160 * 1024;
+    if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
+    auto attr = [&](const void* k, size_t b) -> int {
+        OF3D_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
+        return 0;
+    };
+    int rc = 0;
+    for_each_w_kernel(p->rw, [&](const void* k3_9, const void* k3_5, const void* k4_9, const void* k4_5,
+                                 const void* k5_f, const void* k5_d) {
+        rc |= attr(k3_9, p->k3_lds) | attr(k3_5, p->k3_lds) | attr(k4_9, p->k4_lds) | attr(k4_5, p->k4_lds) |
+              attr(k5_f, p->k5_lds) | attr(k5_d, p->k5_lds);
+    });
+    return rc ? -1 : 0;
 }
+
+// rows of a staged window each thread holds in registers (4 row-groups)
+int nj_bucket(int h) { return h <= 64 ? 16 : (h <= 96 ? 24 : 32); }
 
 struct Ranges {
     int64_t zo0, zo1, zg0, zg1, zb0, zb1;
@@ -587,35 +750,31 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     OF3D_MARK(2);
     double* P = p->ndim == 3 ? p->X : p->Y;
     double* Q = p->ndim == 3 ? p->Y : p->X;
+    const void *k3_9 = nullptr, *k3_5 = nullptr, *k4_9 = nullptr, *k4_5 = nullptr, *k5_f = nullptr, *k5_d = nullptr;
+    for_each_w_kernel(p->rw, [&](const void* a3, const void* b3, const void* a4, const void* b4, const void* a5,
+                                 const void* b5) {
+        k3_9 = a3, k3_5 = b3, k4_9 = a4, k4_5 = b4, k5_f = a5, k5_d = b5;
+    });
+    int rw_arg = p->rw;
     {
-        dim3 g(cdiv(nx, 64), cdiv(ny, 4 * K3_R), ng);
-        if (p->ndim == 3)
-            hipLaunchKernelGGL(k_prod_wy<9>, g, dim3(64, 4), 0, s, G, P, ny, nx, fs, tp.w, tp.rw);
-        else
-            hipLaunchKernelGGL(k_prod_wy<5>, g, dim3(64, 4), 0, s, G, P, ny, nx, fs, tp.w, tp.rw);
-        OF3D_HIP(hipGetLastError());
+        dim3 g(cdiv(nx, 64), cdiv(ny, K3_YC), ng);
+        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
+        OF3D_HIP(hipLaunchKernel(p->ndim == 3 ? k3_9 : k3_5, g, dim3(64, 4), args, p->k3_lds, s));
     }
     OF3D_MARK(3);
     {
-        dim3 g(cdiv(nx, K4_TX), ny, ng);
-        if (p->ndim == 3) {
-            const size_t lds = 9 * (K4_TX + 2 * p->rw) * sizeof(double);
-            hipLaunchKernelGGL(k_wx<9>, g, dim3(256), lds, s, P, Q, ny, nx, fs, tp.w, tp.rw);
-        } else {
-            const size_t lds = 5 * (K4_TX + 2 * p->rw) * sizeof(double);
-            hipLaunchKernelGGL(k_wx<5>, g, dim3(256), lds, s, P, Q, ny, nx, fs, tp.w, tp.rw);
-        }
-        OF3D_HIP(hipGetLastError());
+        dim3 g(cdiv(nx, K4_TX), cdiv(ny, K4_ROWS), ng);
+        void* args[] = {(void*)&P, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
+        OF3D_HIP(hipLaunchKernel(p->ndim == 3 ? k4_9 : k4_5, g, dim3(64, 4), args, p->k4_lds, s));
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {
-        dim3 g(cdiv(nx, 64), cdiv(ny, 4), cdiv(no, K5_R));
-        if (p->rel64)
-            hipLaunchKernelGGL(k_wz_solve<double>, g, dim3(64, 4), 0, s, Q, (int)R.zg0, nz, ny, nx, fs, tp.w, tp.rw,
-                               (int)R.zo0, no, vx, vy, vz, (double*)rel);
-        else
-            hipLaunchKernelGGL(k_wz_solve<float>, g, dim3(64, 4), 0, s, Q, (int)R.zg0, nz, ny, nx, fs, tp.w, tp.rw,
-                               (int)R.zo0, no, vx, vy, vz, (float*)rel);
+        dim3 g(cdiv(nx, 64), ny, cdiv(no, K5_ZC));
+        int zg0 = (int)R.zg0, zo0 = (int)R.zo0;
+        const double* Qc = Q;
+        void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+                        (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
+        OF3D_HIP(hipLaunchKernel(p->rel64 ? k5_d : k5_f, g, dim3(64, 4), args, p->k5_lds, s));
     } else {
         const int n = ny * nx;
         hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);

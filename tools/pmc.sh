@@ -1,0 +1,21 @@
+#!/bin/bash
+# rocprofv3 PMC passes (counters only with --kernel-trace/--stats; one counter group per pass).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
+TAG=${1:-r01}; CFG=${CFG:-c2}; STEPS=${STEPS:-5}
+export TMPDIR=/tmp
+cd /tmp
+if [ -n "${LIST:-}" ]; then timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1; echo "list rc=$?"; fi
+i=0
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+           "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_GROUPS:-}; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/pmc_${CFG}_$TAG/p$i" -o run \
+    -- python3 "$ROOT/bench.py" --config "$CFG" --steps "$STEPS" --warmup 1 --no-cpu-baseline > "$OUT/pmc_${CFG}_${TAG}_p$i.log" 2>&1
+  rc=$?; echo "pass $i ($grp) rc=$rc"
+  case $rc in 0|1|2) ;; *) echo "STOP"; exit $rc;; esac
+done
+exit 0
