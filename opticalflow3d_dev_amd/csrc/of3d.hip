@@ -105,121 +105,6 @@ __device__ __forceinline__ void pass_line(Load ld, int p0, int L, const double* 
     }
 }
 
-// ---------------------------------------------------------------------------
-// K1: temporal derivative + y/x passes of the gradient filters.
-//   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]       (calc_flow.py:279-288, y first)
-//   B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (dz)
-// Tile: K1_TX x-outputs x ty rows of one plane; LDS holds I and dt0 over the
-// (ty+2rd) x (K1_TX+2rd) clamped halo and the three y-pass results.
-// ---------------------------------------------------------------------------
-constexpr int K1_TX = 64;
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_grad_xy(Frames fr, int ty, int ny, int nx, int frames_z0, int zb0,
-                                                 DevTaps tp, double* __restrict__ B, size_t fs, int need_b4) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int rd = tp.rd, rs = tp.rs, rt = tp.rt;
-    const int PW = K1_TX + 2 * rd;
-    const int RH = ty + 2 * rd;
-    double* sI = smem;
-    double* sT = sI + RH * PW;
-    double* sA1 = sT + RH * PW;
-    double* sA2 = sA1 + ty * PW;
-    double* sA3 = sA2 + ty * PW;
-    const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * K1_TX, y0 = blockIdx.y * ty;
-    const int zl = blockIdx.z;
-    const size_t plane = (size_t)(zb0 + zl - frames_z0) * (size_t)ny * nx;
-
-    for (int e = tid; e < RH * PW; e += 256) {
-        const int row = e / PW, col = e - row * PW;
-        const int gy = clampi(y0 - rd + row, 0, ny - 1), gx = clampi(x0 - rd + col, 0, nx - 1);
-        const size_t idx = plane + (size_t)gy * nx + gx;
-        const double c = ldf<T>(fr.p[rt], idx);
-        double dt = c * tp.t[0];
-        for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * tp.t[k];
-        sI[e] = c;
-        sT[e] = dt;
-    }
-    __syncthreads();
-    for (int e = tid; e < ty * PW; e += 256) {
-        const int row = e / PW, col = e - row * PW;
-        const int c = (row + rd) * PW + col;
-        double a1 = sT[c] * tp.g[0], a2 = sI[c] * tp.d[0], a3 = sI[c] * tp.s[0];
-        for (int k = rd; k >= 1; --k) {
-            a1 = a1 + (sT[c - k * PW] + sT[c + k * PW]) * tp.g[k];
-            a2 = a2 + (sI[c - k * PW] - sI[c + k * PW]) * tp.d[k];
-        }
-        for (int k = rs; k >= 1; --k) a3 = a3 + (sI[c - k * PW] + sI[c + k * PW]) * tp.s[k];
-        sA1[e] = a1;
-        sA2[e] = a2;
-        sA3[e] = a3;
-    }
-    __syncthreads();
-    for (int e = tid; e < ty * K1_TX; e += 256) {
-        const int row = e / K1_TX, col = e - row * K1_TX;
-        const int gy = y0 + row, gx = x0 + col;
-        if (gy >= ny || gx >= nx) continue;
-        const int c = row * PW + col + rd;
-        double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
-        for (int k = rd; k >= 1; --k) {
-            b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
-            b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
-        }
-        for (int k = rs; k >= 1; --k) {
-            b2 = b2 + (sA2[c - k] + sA2[c + k]) * tp.s[k];
-            b4 = b4 + (sA3[c - k] + sA3[c + k]) * tp.s[k];
-        }
-        const size_t o = ((size_t)zl * ny + gy) * nx + gx;
-        B[o] = b1;
-        B[fs + o] = b2;
-        B[2 * fs + o] = b3;
-        if (need_b4) B[3 * fs + o] = b4;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K2: z pass of the gradients (calc_flow.py:279-288, last pass, axis 0):
-//   dt = z(G)[B1], dy = z(S)[B2], dx = z(S)[B3], dz = z(D)[B4]
-// ---------------------------------------------------------------------------
-constexpr int K2_R = 4;
-
-__global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, int zb0, double* __restrict__ G,
-                                                int zg0, int nzg, int nz, int ny, int nx, size_t fs, DevTaps tp) {
-    const int x = blockIdx.x * 64 + threadIdx.x, y = blockIdx.y * 4 + threadIdx.y;
-    if (x >= nx || y >= ny) return;
-    const int zl0 = blockIdx.z * K2_R;
-    const int p0 = zg0 + zl0;
-    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + x;
-    const double* b0 = B + col;
-    double out[K2_R];
-    auto store = [&](int f) {
-#pragma unroll
-        for (int i = 0; i < K2_R; ++i)
-            if (zl0 + i < nzg) G[f * fs + (size_t)(zl0 + i) * ps + col] = out[i];
-    };
-    {
-        const double* b = b0;
-        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.g, tp.rd, out);
-        store(0);
-    }
-    {
-        const double* b = b0 + fs;
-        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.s, tp.rs, out);
-        store(1);
-    }
-    {
-        const double* b = b0 + 2 * fs;
-        pass_line<K2_R, false>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.s, tp.rs, out);
-        store(2);
-    }
-    {
-        const double* b = b0 + 3 * fs;
-        pass_line<K2_R, true>([&](int z) { return b[(size_t)(z - zb0) * ps]; }, p0, nz, tp.d, tp.rd, out);
-        store(3);
-    }
-}
-
 // 1-D pass over a staged LDS line, R consecutive outputs per thread at line
 // positions base..base+R-1 (elements `st` doubles apart); the staged line
 // already holds the clamped halo (positions base-r .. base+R-1+r valid).
@@ -267,6 +152,134 @@ __device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, i
 }
 
 // ---------------------------------------------------------------------------
+// K1: temporal derivative + y/x passes of the gradient filters.
+//   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]       (calc_flow.py:279-288, y first)
+//   B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (dz)
+// Block = one 64-wide staged column strip (64 - 2rd output columns) x K1_TY
+// output rows of one plane; lane = staged column.  Stage 0 forms dt0 (T2:
+// centre frame, antisymmetric taps, outer->inner) and I over the clamped
+// halo; the y pass is a ring pass down each lane's column; the x pass reads
+// neighbour columns from LDS.
+// Frames are addressed as base + f*fstride when equally spaced (one stack),
+// else through the pointer table (ring buffer of frames).
+// ---------------------------------------------------------------------------
+constexpr int K1_R = 4, K1_TY = 4 * K1_R;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_grad_xy(Frames fr, long long fstride, int ny, int nx, int frames_z0, int zb0,
+                                                 DevTaps tp, double* __restrict__ B, size_t fs, int need_b4) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int rd = tp.rd, rs = tp.rs, rt = tp.rt;
+    const int RH = K1_TY + 2 * rd;
+    double* sI = smem;
+    double* sT = sI + RH * 64;
+    double* sA1 = sT + RH * 64;
+    double* sA2 = sA1 + K1_TY * 64;
+    double* sA3 = sA2 + K1_TY * 64;
+    const int lane = threadIdx.x, w = threadIdx.y;
+    const int x0 = blockIdx.x * (64 - 2 * rd), y0 = blockIdx.y * K1_TY;
+    const int zl = blockIdx.z;
+    const int gx = clampi(x0 - rd + lane, 0, nx - 1);
+    const size_t plane = (size_t)(zb0 + zl - frames_z0) * (size_t)ny * nx + gx;
+    const T* f0 = reinterpret_cast<const T*>(fr.p[0]);
+    for (int row = w; row < RH; row += 4) {
+        const size_t idx = plane + (size_t)clampi(y0 - rd + row, 0, ny - 1) * nx;
+        double c, dt;
+        if (fstride) {
+            const T* p = f0 + idx;
+            c = (double)p[(long long)rt * fstride];
+            dt = c * tp.t[0];
+            for (int k = rt; k >= 1; --k)
+                dt = dt + ((double)p[(long long)(rt - k) * fstride] - (double)p[(long long)(rt + k) * fstride]) * tp.t[k];
+        } else {
+            c = ldf<T>(fr.p[rt], idx);
+            dt = c * tp.t[0];
+            for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * tp.t[k];
+        }
+        sI[row * 64 + lane] = c;
+        sT[row * 64 + lane] = dt;
+    }
+    __syncthreads();
+    {
+        double a[K1_R];
+        const int base = rd + w * K1_R;
+        lds_pass<K1_R, false>(sT + lane, 64, base, tp.g, rd, a);
+#pragma unroll
+        for (int i = 0; i < K1_R; ++i) sA1[(w * K1_R + i) * 64 + lane] = a[i];
+        lds_pass<K1_R, true>(sI + lane, 64, base, tp.d, rd, a);
+#pragma unroll
+        for (int i = 0; i < K1_R; ++i) sA2[(w * K1_R + i) * 64 + lane] = a[i];
+        lds_pass<K1_R, false>(sI + lane, 64, base, tp.s, rs, a);
+#pragma unroll
+        for (int i = 0; i < K1_R; ++i) sA3[(w * K1_R + i) * 64 + lane] = a[i];
+    }
+    __syncthreads();
+    const int gxo = x0 + lane - rd;
+    if (lane < rd || lane >= 64 - rd || gxo >= nx) return;
+#pragma unroll
+    for (int i = 0; i < K1_R; ++i) {
+        const int row = w * K1_R + i;
+        const int gy = y0 + row;
+        if (gy >= ny) break;
+        const int c = row * 64 + lane;
+        double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
+        for (int k = rd; k >= 1; --k) {
+            b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
+            b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
+        }
+        for (int k = rs; k >= 1; --k) {
+            b2 = b2 + (sA2[c - k] + sA2[c + k]) * tp.s[k];
+            b4 = b4 + (sA3[c - k] + sA3[c + k]) * tp.s[k];
+        }
+        const size_t o = ((size_t)zl * ny + gy) * nx + gxo;
+        B[o] = b1;
+        B[fs + o] = b2;
+        B[2 * fs + o] = b3;
+        if (need_b4) B[3 * fs + o] = b4;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: z pass of the gradients (calc_flow.py:279-288, last pass, axis 0):
+//   dt = z(G)[B1], dy = z(S)[B2], dx = z(S)[B3], dz = z(D)[B4]
+// One field per block: 64 x-columns of one row, K2_ZC output planes; the
+// (K2_ZC + 2r)-plane clamped window is staged in LDS, ring pass per lane.
+// ---------------------------------------------------------------------------
+constexpr int K2_R = 4, K2_ZC = 4 * K2_R;
+
+__global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, int zb0, double* __restrict__ G,
+                                                int zg0, int nzg, int nz, int ny, int nx, size_t fs, DevTaps tp) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int f = blockIdx.z & 3;
+    const int zc = blockIdx.z >> 2;
+    const double* h = f == 0 ? tp.g : (f == 3 ? tp.d : tp.s);
+    const int r = (f == 0 || f == 3) ? tp.rd : tp.rs;
+    const int H = K2_ZC + 2 * r;
+    const int lane = threadIdx.x, g = threadIdx.y;
+    const int x = blockIdx.x * 64 + lane;
+    const int xs = x < nx ? x : nx - 1;
+    const int y = blockIdx.y;
+    const int zc0 = zg0 + zc * K2_ZC;
+    const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + xs;
+    const double* src = B + f * fs + col;
+    for (int row = g; row < H; row += 4)
+        sm[row * 64 + lane] = src[(size_t)(clampi(zc0 - r + row, 0, nz - 1) - zb0) * ps];
+    __syncthreads();
+    double out[K2_R];
+    if (f == 3)
+        lds_pass<K2_R, true>(sm + lane, 64, r + g * K2_R, h, r, out);
+    else
+        lds_pass<K2_R, false>(sm + lane, 64, r + g * K2_R, h, r, out);
+    if (x >= nx) return;
+    double* dst = G + f * fs + (size_t)y * nx + x;
+#pragma unroll
+    for (int i = 0; i < K2_R; ++i) {
+        const int zl = zc0 + g * K2_R + i - zg0;
+        if (zl < nzg) dst[(size_t)zl * ps] = out[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K3: structure-tensor products + W y pass (calc_flow.py:300-313; 2D :133-141).
 // Gradient field index: 0 dt, 1 dy, 2 dx, 3 dz.
 // 3D product order: tx ty tz xy xz x2 yz y2 z2 ;  2D: tx ty xy x2 y2.
@@ -290,48 +303,55 @@ struct ProdTable<5> {
     static constexpr int b[5] = {0, 0, 1, 2, 1};
 };
 
+constexpr int K3_NZB = 4;  // planes per block: next plane's tile is fetched during this plane's pass
+
 template <int NP, int NJ>
-__global__ __launch_bounds__(256, 2) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
-                                                 int nx, size_t fs, const double* __restrict__ hw, int rw) {
+__global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
+                                                 int nx, int nzp, size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int H = K3_YC + 2 * rw;
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
     const int xs = x < nx ? x : nx - 1;
     const int y0 = blockIdx.y * K3_YC;
-    const size_t pl = (size_t)blockIdx.z * ny * nx;
-    double ra[NJ], rb[NJ];
-    // packed product table (4 bits per entry), runtime-indexed
+    const int p = blockIdx.z % NP;
+    const int zb = (blockIdx.z / NP) * K3_NZB;
+    const int nzb = min(K3_NZB, nzp - zb);
+    const size_t ps = (size_t)ny * nx;
+    // packed product table (4 bits per entry)
     constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // a[] = {2,1,3,2,2,2,1,1,3} / {2,1,2,2,1}
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;  // b[] = {0,0,0,1,3,2,3,1,3} / {0,0,1,2,1}
-    auto fetch = [&](int p) {
-        const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
-        const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
+    const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + zb * ps + xs;
+    const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + zb * ps + xs;
+    int roff[NJ];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int row = g + 4 * j;
-            if (row < H) {
-                const size_t o = (size_t)clampi(y0 - rw + row, 0, ny - 1) * nx;
-                ra[j] = ga[o];
-                rb[j] = gb[o];
+    for (int j = 0; j < NJ; ++j) roff[j] = clampi(y0 - rw + g + 4 * j, 0, ny - 1) * nx;
+    double ra[NJ], rb[NJ];
+    auto fetch = [&](int t) {
+        const double* a = ga + t * ps;
+        const double* b = gb + t * ps;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            if (g + 4 * j < H) {
+                ra[j] = a[roff[j]];
+                rb[j] = b[roff[j]];
             }
-        }
     };
     fetch(0);
-#pragma unroll 1
-    for (int p = 0; p < NP; ++p) {
-        double* buf = sm + (p & 1) * H * 64;
+    double* out_base = P + p * fs + zb * ps + x;
+    for (int t = 0; t < nzb; ++t) {
+        if (t) __syncthreads();
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int row = g + 4 * j;
-            if (row < H) buf[row * 64 + lane] = ra[j] * rb[j];
+            if (row < H) sm[row * 64 + lane] = ra[j] * rb[j];
         }
         __syncthreads();
-        if (p + 1 < NP) fetch(p + 1);
+        if (t + 1 < nzb) fetch(t + 1);
         double out[K3_R];
-        lds_pass<K3_R, false>(buf + lane, 64, rw + g * K3_R, hw, rw, out);
+        lds_pass<K3_R, false>(sm + lane, 64, rw + g * K3_R, hw, rw, out);
         if (x < nx) {
-            double* o = P + p * fs + pl + x;
+            double* o = out_base + t * ps;
 #pragma unroll
             for (int i = 0; i < K3_R; ++i) {
                 const int y = y0 + g * K3_R + i;
@@ -347,38 +367,63 @@ __global__ __launch_bounds__(256, 2) void k_prod_wy(const double* __restrict__ G
 // window (K4_R outputs) over an LDS tile of odd pitch (conflict-free column
 // access); results go back through LDS for coalesced row stores.
 // ---------------------------------------------------------------------------
-constexpr int K4_R = 16, K4_TX = 4 * K4_R, K4_ROWS = 64;
+constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64, K4_NZB = 4;
 
-template <int NF>
-__global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
-                                            size_t fs, const double* __restrict__ hw, int rw) {
+// NJ = staged columns per lane: ceil((K4_TX + 2rw) / 64)
+template <int NF, int NJ>
+__global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
+                                            int nzp, size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int W = K4_TX + 2 * rw;
     const int PP = W | 1;
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x0 = blockIdx.x * K4_TX, y0 = blockIdx.y * K4_ROWS;
-    const size_t pl = (size_t)blockIdx.z * ny * nx;
-#pragma unroll 1
-    for (int f = 0; f < NF; ++f) {
-        const double* src = P + f * fs + pl;
-        for (int row = g; row < K4_ROWS; row += 4) {
-            const double* r = src + (size_t)min(y0 + row, ny - 1) * nx;
-            for (int c = lane; c < W; c += 64) sm[row * PP + c] = r[clampi(x0 - rw + c, 0, nx - 1)];
+    const int f = blockIdx.z % NF;
+    const int zb = (blockIdx.z / NF) * K4_NZB;
+    const int nzb = min(K4_NZB, nzp - zb);
+    const size_t ps = (size_t)ny * nx;
+    const double* src = P + f * fs + zb * ps;
+    double* dst = Q + f * fs + zb * ps;
+    int coff[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) coff[j] = clampi(x0 - rw + lane + 64 * j, 0, nx - 1);
+    // 16 staged rows per thread (rows g, g+4, ..., g+60)
+    double rv[16][NJ];
+    auto fetch = [&](int t) {
+        const double* b = src + t * ps;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const double* r = b + (size_t)min(y0 + g + 4 * i, ny - 1) * nx;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (lane + 64 * j < W) rv[i][j] = r[coff[j]];
         }
+    };
+    fetch(0);
+    const int x = x0 + lane;
+    for (int t = 0; t < nzb; ++t) {
+        if (t) __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (lane + 64 * j < W) sm[(g + 4 * i) * PP + lane + 64 * j] = rv[i][j];
         __syncthreads();
+        if (t + 1 < nzb) fetch(t + 1);
         double out[K4_R];
+        // lane = row, 4 groups x K4_R outputs along x
         lds_pass<K4_R, false>(sm + lane * PP, 1, rw + g * K4_R, hw, rw, out);
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < K4_R; ++i) sm[lane * PP + g * K4_R + i] = out[i];
         __syncthreads();
-        double* dst = Q + f * fs + pl;
-        const int x = x0 + lane;
-        for (int row = g; row < K4_ROWS; row += 4) {
-            const int y = y0 + row;
-            if (y < ny && x < nx) dst[(size_t)y * nx + x] = sm[row * PP + lane];
+        if (lane < K4_TX && x < nx) {
+            double* d = dst + t * ps;
+            for (int row = g; row < K4_ROWS; row += 4) {
+                const int y = y0 + row;
+                if (y < ny) d[(size_t)y * nx + x] = sm[row * PP + lane];
+            }
         }
-        __syncthreads();
     }
 }
 
@@ -543,8 +588,7 @@ struct of3d_plan {
     double* Y = nullptr;  // 9 fields
     size_t fs = 0;        // field stride (elements)
     hipStream_t stream = nullptr;
-    int k1_ty = 16;
-    size_t k1_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
+    size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
@@ -607,57 +651,50 @@ DevTaps dev_taps(const of3d_plan* p) {
 unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 template <typename T>
-void launch_k1(dim3 g, size_t lds, hipStream_t s, const Frames& fr, int ty, int ny, int nx, int fz0, int zb0,
+void launch_k1(dim3 g, size_t lds, hipStream_t s, const Frames& fr, long long fstride, int ny, int nx, int fz0, int zb0,
                DevTaps tp, double* B, size_t fs, int need_b4) {
-    hipLaunchKernelGGL(k_grad_xy<T>, g, dim3(256), lds, s, fr, ty, ny, nx, fz0, zb0, tp, B, fs, need_b4);
+    hipLaunchKernelGGL(k_grad_xy<T>, g, dim3(64, 4), lds, s, fr, fstride, ny, nx, fz0, zb0, tp, B, fs, need_b4);
 }
 
-// W-pass kernel variants: rows of a staged window each thread prefetches
-// into registers (4 row-groups) — NJ >= ceil(H/4).
+// K5 variants: rows of the staged window each thread prefetches into
+// registers (4 row-groups): NJ >= ceil(H/4).
 int nj_for(int h) { return h <= 64 ? 16 : (h <= 80 ? 20 : (h <= 96 ? 24 : 32)); }
 
-template <int NJ3, int NJ5>
-struct WKernels {
-    static const void* k3_9() { return (const void*)k_prod_wy<9, NJ3>; }
-    static const void* k3_5() { return (const void*)k_prod_wy<5, NJ3>; }
-    static const void* k4_9() { return (const void*)k_wx<9>; }
-    static const void* k4_5() { return (const void*)k_wx<5>; }
-    static const void* k5_f() { return (const void*)k_wz_solve<float, NJ5>; }
-    static const void* k5_d() { return (const void*)k_wz_solve<double, NJ5>; }
-};
-
-template <typename F>
-void for_each_w_kernel(int rw, F&& f) {
-    auto call = [&](auto K) { f(K.k3_9(), K.k3_5(), K.k4_9(), K.k4_5(), K.k5_f(), K.k5_d()); };
-    const int nj3 = nj_for(K3_YC + 2 * rw), nj5 = nj_for(K5_ZC + 2 * rw);
-    if (nj3 == 16 && nj5 == 16) call(WKernels<16, 16>{});
-    else if (nj3 == 20 && nj5 == 16) call(WKernels<20, 16>{});
-    else if (nj3 == 24 && nj5 == 16) call(WKernels<24, 16>{});
-    else if (nj3 == 24 && nj5 == 20) call(WKernels<24, 20>{});
-    else if (nj3 == 24 && nj5 == 24) call(WKernels<24, 24>{});
-    else if (nj3 == 32 && nj5 == 24) call(WKernels<32, 24>{});
-    else call(WKernels<32, 32>{});
+template <typename RelT>
+const void* k5_kernel(int rw) {
+    switch (nj_for(K5_ZC + 2 * rw)) {
+        case 16: return (const void*)k_wz_solve<RelT, 16>;
+        case 20: return (const void*)k_wz_solve<RelT, 20>;
+        case 24: return (const void*)k_wz_solve<RelT, 24>;
+        default: return (const void*)k_wz_solve<RelT, 32>;
+    }
 }
 
-int set_k1_attrs(of3d_plan* p) {
-    // pick the tallest tile whose LDS footprint fits
-    for (int ty : {16, 8, 4, 2, 1}) {
-        const size_t pw = K1_TX + 2 * p->rd, rh = ty + 2 * p->rd;
-        const size_t bytes = (2 * rh * pw + 3 * (size_t)ty * pw) * sizeof(double);
-        if (bytes <= 160 * 1024) {
-            p->k1_ty = ty;
-            p->k1_lds = bytes;
-            break;
-        }
-        if (ty == 1) return fail("of3d: xyzSig too large for the LDS tile");
+const void* k3_kernel(int np, int rw) {
+    const int nj = nj_for(K3_YC + 2 * rw);
+#define K3K(NP)                                                       \
+    switch (nj) {                                                     \
+        case 16: return (const void*)k_prod_wy<NP, 16>;               \
+        case 20: return (const void*)k_prod_wy<NP, 20>;               \
+        case 24: return (const void*)k_prod_wy<NP, 24>;               \
+        default: return (const void*)k_prod_wy<NP, 32>;               \
     }
-    const void* ks[] = {(const void*)k_grad_xy<uint8_t>,  (const void*)k_grad_xy<uint16_t>,
-                        (const void*)k_grad_xy<int16_t>,  (const void*)k_grad_xy<uint32_t>,
-                        (const void*)k_grad_xy<int32_t>,  (const void*)k_grad_xy<float>,
-                        (const void*)k_grad_xy<double>};
-    for (auto k : ks) OF3D_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k1_lds));
-    // W-pass tiles
-    p->k3_lds = (size_t)2 * (K3_YC + 2 * p->rw) * 64 * sizeof(double);
+    if (np == 9) { K3K(9) } else { K3K(5) }
+#undef K3K
+}
+
+const void* k4_kernel(int nf, int rw) {
+    const int nj = (K4_TX + 2 * rw + 63) / 64;
+    if (nf == 9) return nj <= 1 ? (const void*)k_wx<9, 1> : (const void*)k_wx<9, 2>;
+    return nj <= 1 ? (const void*)k_wx<5, 1> : (const void*)k_wx<5, 2>;
+}
+
+int set_attrs(of3d_plan* p) {
+    if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
+    if (K4_TX + 2 * p->rw > 128) return fail("of3d: wSig too large (window radius > 48)");
+    p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * sizeof(double);
+    p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
+    p->k3_lds = (size_t)(K3_YC + 2 * p->rw) * 64 * sizeof(double);
     p->k4_lds = (size_t)K4_ROWS * ((K4_TX + 2 * p->rw) | 1) * sizeof(double);
     p->k5_lds = (size_t)2 * (K5_ZC + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
@@ -667,16 +704,16 @@ int set_k1_attrs(of3d_plan* p) {
         return 0;
     };
     int rc = 0;
-    for_each_w_kernel(p->rw, [&](const void* k3_9, const void* k3_5, const void* k4_9, const void* k4_5,
-                                 const void* k5_f, const void* k5_d) {
-        rc |= attr(k3_9, p->k3_lds) | attr(k3_5, p->k3_lds) | attr(k4_9, p->k4_lds) | attr(k4_5, p->k4_lds) |
-              attr(k5_f, p->k5_lds) | attr(k5_d, p->k5_lds);
-    });
+    rc |= attr((const void*)k_grad_xy<uint8_t>, p->k1_lds) | attr((const void*)k_grad_xy<uint16_t>, p->k1_lds) |
+          attr((const void*)k_grad_xy<int16_t>, p->k1_lds) | attr((const void*)k_grad_xy<uint32_t>, p->k1_lds) |
+          attr((const void*)k_grad_xy<int32_t>, p->k1_lds) | attr((const void*)k_grad_xy<float>, p->k1_lds) |
+          attr((const void*)k_grad_xy<double>, p->k1_lds);
+    rc |= attr((const void*)k_grad_z, p->k2_lds);
+    rc |= attr(k3_kernel(9, p->rw), p->k3_lds) | attr(k3_kernel(5, p->rw), p->k3_lds);
+    rc |= attr(k4_kernel(9, p->rw), p->k4_lds) | attr(k4_kernel(5, p->rw), p->k4_lds);
+    rc |= attr(k5_kernel<float>(p->rw), p->k5_lds) | attr(k5_kernel<double>(p->rw), p->k5_lds);
     return rc ? -1 : 0;
 }
-
-// rows of a staged window each thread holds in registers (4 row-groups)
-int nj_bucket(int h) { return h <= 64 ? 16 : (h <= 96 ? 24 : 32); }
 
 struct Ranges {
     int64_t zo0, zo1, zg0, zg1, zb0, zb1;
@@ -722,26 +759,37 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         if (evs) OF3D_HIP(hipEventRecord(evs[i], s)); \
     } while (0)
     OF3D_MARK(0);
-    // K1
+    // K1 — frames equally spaced (one stack) are addressed by stride
     {
-        dim3 g(cdiv(nx, K1_TX), cdiv(ny, p->k1_ty), nb);
+        const size_t es = dtype_size(dtype);
+        long long fstride = 0;
+        const int nwin = 2 * p->rt + 1;
+        if (nwin > 1) {
+            const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
+            bool eq = d > 0 && d % (long long)es == 0;
+            for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
+            if (eq) fstride = d / (long long)es;
+        }
+        dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), nb);
         const int fz0 = (int)frame_z0, zb0 = (int)R.zb0, need_b4 = p->ndim == 3;
+        const size_t L = p->k1_lds;
         switch (dtype) {
-            case OF3D_U8: launch_k1<uint8_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_U16: launch_k1<uint16_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_I16: launch_k1<int16_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_U32: launch_k1<uint32_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_I32: launch_k1<int32_t>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_F32: launch_k1<float>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_F64: launch_k1<double>(g, p->k1_lds, s, fr, p->k1_ty, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_U8: launch_k1<uint8_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_U16: launch_k1<uint16_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_I16: launch_k1<int16_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_U32: launch_k1<uint32_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_I32: launch_k1<int32_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_F32: launch_k1<float>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+            case OF3D_F64: launch_k1<double>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
         }
         OF3D_HIP(hipGetLastError());
     }
     OF3D_MARK(1);
     const double* G;
     if (p->ndim == 3) {
-        dim3 g(cdiv(nx, 64), cdiv(ny, 4), cdiv(ng, K2_R));
-        hipLaunchKernelGGL(k_grad_z, g, dim3(64, 4), 0, s, p->X, (int)R.zb0, p->Y, (int)R.zg0, ng, nz, ny, nx, fs, tp);
+        dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
+        hipLaunchKernelGGL(k_grad_z, g, dim3(64, 4), p->k2_lds, s, p->X, (int)R.zb0, p->Y, (int)R.zg0, ng, nz, ny, nx,
+                           fs, tp);
         OF3D_HIP(hipGetLastError());
         G = p->Y;
     } else {
@@ -750,31 +798,32 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     OF3D_MARK(2);
     double* P = p->ndim == 3 ? p->X : p->Y;
     double* Q = p->ndim == 3 ? p->Y : p->X;
-    const void *k3_9 = nullptr, *k3_5 = nullptr, *k4_9 = nullptr, *k4_5 = nullptr, *k5_f = nullptr, *k5_d = nullptr;
-    for_each_w_kernel(p->rw, [&](const void* a3, const void* b3, const void* a4, const void* b4, const void* a5,
-                                 const void* b5) {
-        k3_9 = a3, k3_5 = b3, k4_9 = a4, k4_5 = b4, k5_f = a5, k5_d = b5;
-    });
-    int rw_arg = p->rw;
+    const int nf = p->ndim == 3 ? 9 : 5;
     {
-        dim3 g(cdiv(nx, 64), cdiv(ny, K3_YC), ng);
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(p->ndim == 3 ? k3_9 : k3_5, g, dim3(64, 4), args, p->k3_lds, s));
+        dim3 g(cdiv(nx, 64), cdiv(ny, K3_YC), cdiv(ng, K3_NZB) * nf);
+        int rw_arg = p->rw, ng_arg = ng;
+        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&ng_arg, (void*)&fs, (void*)&tp.w,
+                        (void*)&rw_arg};
+        OF3D_HIP(hipLaunchKernel(k3_kernel(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
     }
     OF3D_MARK(3);
     {
-        dim3 g(cdiv(nx, K4_TX), cdiv(ny, K4_ROWS), ng);
-        void* args[] = {(void*)&P, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(p->ndim == 3 ? k4_9 : k4_5, g, dim3(64, 4), args, p->k4_lds, s));
+        dim3 g(cdiv(nx, K4_TX), cdiv(ny, K4_ROWS), cdiv(ng, K4_NZB) * nf);
+        int rw_arg = p->rw, ng_arg = ng;
+        const double* Pc = P;
+        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&ng_arg, (void*)&fs, (void*)&tp.w,
+                        (void*)&rw_arg};
+        OF3D_HIP(hipLaunchKernel(k4_kernel(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {
         dim3 g(cdiv(nx, 64), ny, cdiv(no, K5_ZC));
-        int zg0 = (int)R.zg0, zo0 = (int)R.zo0;
+        int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
         const double* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-        OF3D_HIP(hipLaunchKernel(p->rel64 ? k5_d : k5_f, g, dim3(64, 4), args, p->k5_lds, s));
+        const void* k5 = p->rel64 ? k5_kernel<double>(p->rw) : k5_kernel<float>(p->rw);
+        OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, 4), args, p->k5_lds, s));
     } else {
         const int n = ny * nx;
         hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);
@@ -805,7 +854,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->device = device;
     if (build_taps(taps, p.get())) return -1;
     OF3D_HIP(hipSetDevice(device));
-    if (set_k1_attrs(p.get())) return -1;
+    if (set_attrs(p.get())) return -1;
     int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
     p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
     p->fs = (size_t)p->cap_planes * ny * nx;

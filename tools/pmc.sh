@@ -1,17 +1,18 @@
 #!/bin/bash
-# rocprofv3 PMC passes (counters only with --kernel-trace/--stats; one counter group per pass).
+# rocprofv3 PMC passes (counters only with --kernel-trace; one counter group per pass).
+# PMC_GROUPS: ';'-separated counter groups (default below).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
 TAG=${1:-r01}; CFG=${CFG:-c2}; STEPS=${STEPS:-5}
+DEF="FETCH_SIZE;WRITE_SIZE;SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_LDS SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVES GRBM_GUI_ACTIVE;SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAIT_INST_LDS;TCC_HIT_sum TCC_MISS_sum"
+GROUPS_=${PMC_GROUPS:-$DEF}
 export TMPDIR=/tmp
 cd /tmp
 if [ -n "${LIST:-}" ]; then timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1; echo "list rc=$?"; fi
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM" \
-           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
-           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
-           "TCC_HIT_sum TCC_MISS_sum" ${EXTRA_GROUPS:-}; do
+IFS=';' read -ra GRP <<< "$GROUPS_"
+for grp in "${GRP[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/pmc_${CFG}_$TAG/p$i" -o run \
     -- python3 "$ROOT/bench.py" --config "$CFG" --steps "$STEPS" --warmup 1 --no-cpu-baseline > "$OUT/pmc_${CFG}_${TAG}_p$i.log" 2>&1
