@@ -112,64 +112,95 @@ __device__ __forceinline__ void pass_line(Load ld, int p0, int L, const double* 
 //
 // Register reuse without register moves: at step q (k = r-q) output i needs
 // lo = s[base-r+q+i] and hi = s[base+r-q+i].  Both are streams indexed by
-// (q+i) and (q-i); each lives in an R-slot ring (L[m % R], U[m % R]), and
-// the q loop is unrolled by R so every slot index is a compile-time constant.
+// (q+i) and (q-i); each lives in a ring of M slots (L[m % M], U[m % M]), and
+// the q loop is unrolled by M so every slot index is a compile-time constant.
 // Per step: 2 LDS reads, 3R fp64 ops, ~3R live doubles, any radius.
-template <int R, bool ANTI>
+template <int R, bool ANTI, int D = 1, bool WRAP = false>
 __device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, int base,
-                                         const double* __restrict__ h, int r, double (&out)[R]) {
-    double L[R], U[R];
+                                         const double* __restrict__ h, int r, double (&out)[R], int wmask = 0) {
+    // WRAP: the staged line is a ring of (wmask + 1) positions (power of two)
+    auto at = [&](int i) { return WRAP ? s[(i & wmask) * st] : s[i * st]; };
+    // Ring of M = R + D - 1 slots per stream: the two reads issued after step q
+    // are first consumed at step q + D (prefetch distance D hides LDS latency).
+    constexpr int M = R + D - 1;
+    double L[M], U[M];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        out[i] = s[(base + i) * st] * h[0];
-        L[i] = s[(base - r + i) * st];                   // S_lo[i]
-        U[(R - i) % R] = s[(base + r + i) * st];        // S_hi[-i]  -> slot (-i mod R)
-    }
-    // one step q (k = r - q) with ring phase j = q mod R (compile-time)
-    auto step = [&](int q, auto jc) {
+    for (int i = 0; i < R; ++i) out[i] = at(base + i) * h[0];
+#pragma unroll
+    for (int m = 0; m < M; ++m) L[m] = at(base - r + m);           // S_lo[0 .. M-1]
+#pragma unroll
+    for (int m = -(R - 1); m < D; ++m) U[((m % M) + M) % M] = at(base + r - m);  // S_hi[-(R-1) .. D-1]
+    auto step = [&](int q, auto jc) {  // phase j = q mod M (compile-time)
         constexpr int j = decltype(jc)::value;
         const double wk = h[r - q];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            const double lo = L[(i + j) % R];
-            const double hi = U[(j - i + R) % R];
+            const double lo = L[(j + i) % M];
+            const double hi = U[((j - i) % M + M) % M];
             out[i] = out[i] + (ANTI ? (lo - hi) : (lo + hi)) * wk;
         }
-        // refill (always inside the staged window, also after the last step)
-        L[j] = s[(base - r + q + R) * st];           // S_lo[q+R]
-        U[(j + 1) % R] = s[(base + r - q - 1) * st];  // S_hi[q+1]
+        L[j] = at(base - r + q + M);           // S_lo[q+M]   (slot of S_lo[q], done)
+        U[(j + D) % M] = at(base + r - q - D);  // S_hi[q+D]   (slot of S_hi[q-R+1], done)
     };
     int q = 0;
-    for (; q + R <= r; q += R) {
+    for (; q + M <= r; q += M) {
         [&]<int... J>(std::integer_sequence<int, J...>) {
             (step(q + J, std::integral_constant<int, J>{}), ...);
-        }(std::make_integer_sequence<int, R>{});
+        }(std::make_integer_sequence<int, M>{});
     }
-    const int t = r - q;  // 0 .. R-1 remaining steps, phases 0 .. t-1
+    const int t = r - q;  // 0 .. M-1 remaining steps
     [&]<int... J>(std::integer_sequence<int, J...>) {
         ((J < t ? step(q + J, std::integral_constant<int, J>{}) : void()), ...);
-    }(std::make_integer_sequence<int, R - 1>{});
+    }(std::make_integer_sequence<int, M - 1>{});
 }
 
 // ---------------------------------------------------------------------------
-// K1: temporal derivative + y/x passes of the gradient filters.
-//   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]       (calc_flow.py:279-288, y first)
+// K0: temporal derivative of the centre frame (T2, calc_flow.py:276-277):
+//   dt0 = I[c]*T[0] + sum_{k=rt..1} (I[c-k] - I[c+k]) * T[k]
+// (scipy's antisymmetric order, outer tap first; the reference filters all Nt
+// frames and keeps the centre — only the centre line is formed here).
+// Streaming, one voxel per lane; frames by stride (one stack) or pointer table.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_tderiv(Frames fr, long long fstride, size_t off0, size_t n, int rt,
+                                                const double* __restrict__ ht, double* __restrict__ D0) {
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) {
+        const size_t idx = off0 + i;
+        double c, dt;
+        if (fstride) {
+            const T* p = reinterpret_cast<const T*>(fr.p[0]) + idx;
+            c = (double)p[(long long)rt * fstride];
+            dt = c * ht[0];
+            for (int k = rt; k >= 1; --k)
+                dt = dt + ((double)p[(long long)(rt - k) * fstride] - (double)p[(long long)(rt + k) * fstride]) * ht[k];
+        } else {
+            c = ldf<T>(fr.p[rt], idx);
+            dt = c * ht[0];
+            for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * ht[k];
+        }
+        D0[i] = dt;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1: y and x passes of the gradient filters (calc_flow.py:279-288, y first):
+//   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]
 //   B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (dz)
 // Block = one 64-wide staged column strip (64 - 2rd output columns) x K1_TY
-// output rows of one plane; lane = staged column.  Stage 0 forms dt0 (T2:
-// centre frame, antisymmetric taps, outer->inner) and I over the clamped
-// halo; the y pass is a ring pass down each lane's column; the x pass reads
-// neighbour columns from LDS.
-// Frames are addressed as base + f*fstride when equally spaced (one stack),
-// else through the pointer table (ring buffer of frames).
+// output rows, walking K1_NZB planes; lane = staged column.  The next plane's
+// I / dt0 rows are fetched into registers during this plane's passes.  The y
+// pass is a ring pass down each lane's column; the x pass reads neighbour
+// columns from LDS.
 // ---------------------------------------------------------------------------
-constexpr int K1_R = 4, K1_TY = 4 * K1_R;
+constexpr int K1_R = 4, K1_TY = 4 * K1_R, K1_NZB = 4;
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_grad_xy(Frames fr, long long fstride, int ny, int nx, int frames_z0, int zb0,
-                                                 DevTaps tp, double* __restrict__ B, size_t fs, int need_b4) {
+template <typename T, int NJ>
+__global__ __launch_bounds__(256) void k_grad_xy(const T* __restrict__ Ic, const double* __restrict__ D0, int ny,
+                                                 int nx, int nzp, DevTaps tp, double* __restrict__ B, size_t fs,
+                                                 int need_b4) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int rd = tp.rd, rs = tp.rs, rt = tp.rt;
+    const int rd = tp.rd, rs = tp.rs;
     const int RH = K1_TY + 2 * rd;
     double* sI = smem;
     double* sT = sI + RH * 64;
@@ -178,64 +209,77 @@ __global__ __launch_bounds__(256) void k_grad_xy(Frames fr, long long fstride, i
     double* sA3 = sA2 + K1_TY * 64;
     const int lane = threadIdx.x, w = threadIdx.y;
     const int x0 = blockIdx.x * (64 - 2 * rd), y0 = blockIdx.y * K1_TY;
-    const int zl = blockIdx.z;
+    const int zb = blockIdx.z * K1_NZB;
+    const int nzb = min(K1_NZB, nzp - zb);
+    const size_t ps = (size_t)ny * nx;
     const int gx = clampi(x0 - rd + lane, 0, nx - 1);
-    const size_t plane = (size_t)(zb0 + zl - frames_z0) * (size_t)ny * nx + gx;
-    const T* f0 = reinterpret_cast<const T*>(fr.p[0]);
-    for (int row = w; row < RH; row += 4) {
-        const size_t idx = plane + (size_t)clampi(y0 - rd + row, 0, ny - 1) * nx;
-        double c, dt;
-        if (fstride) {
-            const T* p = f0 + idx;
-            c = (double)p[(long long)rt * fstride];
-            dt = c * tp.t[0];
-            for (int k = rt; k >= 1; --k)
-                dt = dt + ((double)p[(long long)(rt - k) * fstride] - (double)p[(long long)(rt + k) * fstride]) * tp.t[k];
-        } else {
-            c = ldf<T>(fr.p[rt], idx);
-            dt = c * tp.t[0];
-            for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * tp.t[k];
-        }
-        sI[row * 64 + lane] = c;
-        sT[row * 64 + lane] = dt;
-    }
-    __syncthreads();
-    {
-        double a[K1_R];
-        const int base = rd + w * K1_R;
-        lds_pass<K1_R, false>(sT + lane, 64, base, tp.g, rd, a);
+    int roff[NJ];
 #pragma unroll
-        for (int i = 0; i < K1_R; ++i) sA1[(w * K1_R + i) * 64 + lane] = a[i];
-        lds_pass<K1_R, true>(sI + lane, 64, base, tp.d, rd, a);
+    for (int j = 0; j < NJ; ++j) roff[j] = clampi(y0 - rd + w + 4 * j, 0, ny - 1) * nx + gx;
+    double rI[NJ], rT[NJ];
+    auto fetch = [&](int t) {
+        const T* ip = Ic + (size_t)(zb + t) * ps;
+        const double* dp = D0 + (size_t)(zb + t) * ps;
 #pragma unroll
-        for (int i = 0; i < K1_R; ++i) sA2[(w * K1_R + i) * 64 + lane] = a[i];
-        lds_pass<K1_R, false>(sI + lane, 64, base, tp.s, rs, a);
-#pragma unroll
-        for (int i = 0; i < K1_R; ++i) sA3[(w * K1_R + i) * 64 + lane] = a[i];
-    }
-    __syncthreads();
+        for (int j = 0; j < NJ; ++j)
+            if (w + 4 * j < RH) {
+                rI[j] = (double)ip[roff[j]];
+                rT[j] = dp[roff[j]];
+            }
+    };
+    fetch(0);
     const int gxo = x0 + lane - rd;
-    if (lane < rd || lane >= 64 - rd || gxo >= nx) return;
+    const bool xout = lane >= rd && lane < 64 - rd && gxo < nx;
+    for (int t = 0; t < nzb; ++t) {
 #pragma unroll
-    for (int i = 0; i < K1_R; ++i) {
-        const int row = w * K1_R + i;
-        const int gy = y0 + row;
-        if (gy >= ny) break;
-        const int c = row * 64 + lane;
-        double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
-        for (int k = rd; k >= 1; --k) {
-            b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
-            b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
+        for (int j = 0; j < NJ; ++j) {
+            const int row = w + 4 * j;
+            if (row < RH) {
+                sI[row * 64 + lane] = rI[j];
+                sT[row * 64 + lane] = rT[j];
+            }
         }
-        for (int k = rs; k >= 1; --k) {
-            b2 = b2 + (sA2[c - k] + sA2[c + k]) * tp.s[k];
-            b4 = b4 + (sA3[c - k] + sA3[c + k]) * tp.s[k];
+        __syncthreads();
+        if (t + 1 < nzb) fetch(t + 1);
+        {
+            double a[K1_R];
+            const int base = rd + w * K1_R;
+            lds_pass<K1_R, false>(sT + lane, 64, base, tp.g, rd, a);
+#pragma unroll
+            for (int i = 0; i < K1_R; ++i) sA1[(w * K1_R + i) * 64 + lane] = a[i];
+            lds_pass<K1_R, true>(sI + lane, 64, base, tp.d, rd, a);
+#pragma unroll
+            for (int i = 0; i < K1_R; ++i) sA2[(w * K1_R + i) * 64 + lane] = a[i];
+            lds_pass<K1_R, false>(sI + lane, 64, base, tp.s, rs, a);
+#pragma unroll
+            for (int i = 0; i < K1_R; ++i) sA3[(w * K1_R + i) * 64 + lane] = a[i];
         }
-        const size_t o = ((size_t)zl * ny + gy) * nx + gxo;
-        B[o] = b1;
-        B[fs + o] = b2;
-        B[2 * fs + o] = b3;
-        if (need_b4) B[3 * fs + o] = b4;
+        __syncthreads();
+        if (xout) {
+            double* bp = B + (size_t)(zb + t) * ps + gxo;
+#pragma unroll
+            for (int i = 0; i < K1_R; ++i) {
+                const int row = w * K1_R + i;
+                const int gy = y0 + row;
+                if (gy >= ny) break;
+                const int c = row * 64 + lane;
+                double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
+                for (int k = rd; k >= 1; --k) {
+                    b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
+                    b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
+                }
+                for (int k = rs; k >= 1; --k) {
+                    b2 = b2 + (sA2[c - k] + sA2[c + k]) * tp.s[k];
+                    b4 = b4 + (sA3[c - k] + sA3[c + k]) * tp.s[k];
+                }
+                const size_t o = (size_t)gy * nx;
+                bp[o] = b1;
+                bp[fs + o] = b2;
+                bp[2 * fs + o] = b3;
+                if (need_b4) bp[3 * fs + o] = b4;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -303,61 +347,61 @@ struct ProdTable<5> {
     static constexpr int b[5] = {0, 0, 1, 2, 1};
 };
 
-constexpr int K3_NZB = 4;  // planes per block: next plane's tile is fetched during this plane's pass
+// Streaming form: a block owns one 64-column strip of one plane and one
+// product, and marches down the whole column height K3_STEP rows at a time.
+// Product rows live in an LDS ring of HR rows (power of two >= K3_STEP + 2rw),
+// keyed by y' = y + rw, so every product row is loaded once; the next step's
+// rows are fetched into registers while the current step's pass runs.
+constexpr int K3_STEP = K3_YC;
 
-template <int NP, int NJ>
+template <int NP, int HR>
 __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
-                                                 int nx, int nzp, size_t fs, const double* __restrict__ hw, int rw) {
+                                                 int nx, size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int H = K3_YC + 2 * rw;
+    constexpr int NJ = K3_STEP / 4;  // rows per thread per step
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
     const int xs = x < nx ? x : nx - 1;
-    const int y0 = blockIdx.y * K3_YC;
     const int p = blockIdx.z % NP;
-    const int zb = (blockIdx.z / NP) * K3_NZB;
-    const int nzb = min(K3_NZB, nzp - zb);
-    const size_t ps = (size_t)ny * nx;
+    const size_t pl = (size_t)(blockIdx.z / NP) * ny * nx;
     // packed product table (4 bits per entry)
     constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // a[] = {2,1,3,2,2,2,1,1,3} / {2,1,2,2,1}
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;  // b[] = {0,0,0,1,3,2,3,1,3} / {0,0,1,2,1}
-    const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + zb * ps + xs;
-    const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + zb * ps + xs;
-    int roff[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) roff[j] = clampi(y0 - rw + g + 4 * j, 0, ny - 1) * nx;
-    double ra[NJ], rb[NJ];
-    auto fetch = [&](int t) {
-        const double* a = ga + t * ps;
-        const double* b = gb + t * ps;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            if (g + 4 * j < H) {
-                ra[j] = a[roff[j]];
-                rb[j] = b[roff[j]];
-            }
+    const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
+    const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
+    auto prod = [&](int yp) {  // product at ring key y' (clamped row y' - rw)
+        const size_t o = (size_t)clampi(yp - rw, 0, ny - 1) * nx;
+        return ga[o] * gb[o];
     };
-    fetch(0);
-    double* out_base = P + p * fs + zb * ps + x;
-    for (int t = 0; t < nzb; ++t) {
-        if (t) __syncthreads();
+    // prologue: rows y' in [0, 2rw) directly, rows [2rw, 2rw + STEP) into registers
+    for (int yp = g; yp < 2 * rw; yp += 4) sm[(yp & (HR - 1)) * 64 + lane] = prod(yp);
+    double ra[NJ], rb[NJ];
+    auto fetch = [&](int yp0) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int row = g + 4 * j;
-            if (row < H) sm[row * 64 + lane] = ra[j] * rb[j];
+            const size_t o = (size_t)clampi(yp0 + g + 4 * j - rw, 0, ny - 1) * nx;
+            ra[j] = ga[o];
+            rb[j] = gb[o];
         }
+    };
+    fetch(2 * rw);
+    double* o = P + p * fs + pl + x;
+    for (int y0 = 0; y0 < ny; y0 += K3_STEP) {
+        // rows y' in [y0 + 2rw, y0 + 2rw + STEP) enter the ring
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sm[((y0 + 2 * rw + g + 4 * j) & (HR - 1)) * 64 + lane] = ra[j] * rb[j];
         __syncthreads();
-        if (t + 1 < nzb) fetch(t + 1);
+        if (y0 + K3_STEP < ny) fetch(y0 + K3_STEP + 2 * rw);
         double out[K3_R];
-        lds_pass<K3_R, false>(sm + lane, 64, rw + g * K3_R, hw, rw, out);
+        lds_pass<K3_R, false, 1, true>(sm + lane, 64, y0 + rw + g * K3_R, hw, rw, out, HR - 1);
         if (x < nx) {
-            double* o = out_base + t * ps;
 #pragma unroll
             for (int i = 0; i < K3_R; ++i) {
                 const int y = y0 + g * K3_R + i;
                 if (y < ny) o[(size_t)y * nx] = out[i];
             }
         }
+        __syncthreads();
     }
 }
 
@@ -367,63 +411,57 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
 // window (K4_R outputs) over an LDS tile of odd pitch (conflict-free column
 // access); results go back through LDS for coalesced row stores.
 // ---------------------------------------------------------------------------
-constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64, K4_NZB = 4;
+constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64;
 
-// NJ = staged columns per lane: ceil((K4_TX + 2rw) / 64)
-template <int NF, int NJ>
+// Streaming form: a block owns 64 rows of one plane and one field, and marches
+// along x K4_TX columns at a time; columns live in an LDS ring of HC columns
+// (power of two >= K4_TX + 2rw, keyed by x' = x + rw, odd row pitch HC + 1 so
+// lane = row reads are conflict-free).  Results leave through a transposing
+// LDS tile for coalesced row stores; the next step's columns are fetched into
+// registers during the current pass.
+template <int NF, int HC>
 __global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
-                                            int nzp, size_t fs, const double* __restrict__ hw, int rw) {
+                                            size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int W = K4_TX + 2 * rw;
-    const int PP = W | 1;
+    constexpr int PP = HC + 1;
+    constexpr int OP = K4_TX + 1;
+    double* so = sm + K4_ROWS * PP;  // output tile [row][K4_TX]
     const int lane = threadIdx.x, g = threadIdx.y;
-    const int x0 = blockIdx.x * K4_TX, y0 = blockIdx.y * K4_ROWS;
+    const int y0 = blockIdx.y * K4_ROWS;
     const int f = blockIdx.z % NF;
-    const int zb = (blockIdx.z / NF) * K4_NZB;
-    const int nzb = min(K4_NZB, nzp - zb);
-    const size_t ps = (size_t)ny * nx;
-    const double* src = P + f * fs + zb * ps;
-    double* dst = Q + f * fs + zb * ps;
-    int coff[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) coff[j] = clampi(x0 - rw + lane + 64 * j, 0, nx - 1);
-    // 16 staged rows per thread (rows g, g+4, ..., g+60)
-    double rv[16][NJ];
-    auto fetch = [&](int t) {
-        const double* b = src + t * ps;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const double* r = b + (size_t)min(y0 + g + 4 * i, ny - 1) * nx;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (lane + 64 * j < W) rv[i][j] = r[coff[j]];
-        }
+    const size_t pl = (size_t)(blockIdx.z / NF) * ny * nx;
+    const double* src = P + f * fs + pl;
+    double* dst = Q + f * fs + pl;
+    // loader mapping: lanes 0..31 / 32..63 -> two rows, 32 consecutive columns
+    const int lc = lane & 31, lr = (lane >> 5) + 2 * g;  // rows lr, lr + 8, ..., lr + 56
+    auto colv = [&](int row, int xp) {
+        return src[(size_t)min(y0 + row, ny - 1) * nx + clampi(xp - rw, 0, nx - 1)];
     };
-    fetch(0);
-    const int x = x0 + lane;
-    for (int t = 0; t < nzb; ++t) {
-        if (t) __syncthreads();
+    for (int xp = lc; xp < 2 * rw; xp += 32)
+        for (int row = lr; row < K4_ROWS; row += 8) sm[row * PP + (xp & (HC - 1))] = colv(row, xp);
+    double rv[8];
+    auto fetch = [&](int xp0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < 8; ++j) rv[j] = colv(lr + 8 * j, xp0 + lc);
+    };
+    fetch(2 * rw);
+    for (int x0 = 0; x0 < nx; x0 += K4_TX) {
 #pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (lane + 64 * j < W) sm[(g + 4 * i) * PP + lane + 64 * j] = rv[i][j];
+        for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + ((x0 + 2 * rw + lc) & (HC - 1))] = rv[j];
         __syncthreads();
-        if (t + 1 < nzb) fetch(t + 1);
+        if (x0 + K4_TX < nx) fetch(x0 + K4_TX + 2 * rw);
         double out[K4_R];
-        // lane = row, 4 groups x K4_R outputs along x
-        lds_pass<K4_R, false>(sm + lane * PP, 1, rw + g * K4_R, hw, rw, out);
-        __syncthreads();
+        lds_pass<K4_R, false, 1, true>(sm + lane * PP, 1, x0 + rw + g * K4_R, hw, rw, out, HC - 1);
 #pragma unroll
-        for (int i = 0; i < K4_R; ++i) sm[lane * PP + g * K4_R + i] = out[i];
+        for (int i = 0; i < K4_R; ++i) so[lane * OP + g * K4_R + i] = out[i];
         __syncthreads();
-        if (lane < K4_TX && x < nx) {
-            double* d = dst + t * ps;
-            for (int row = g; row < K4_ROWS; row += 4) {
-                const int y = y0 + row;
-                if (y < ny) d[(size_t)y * nx + x] = sm[row * PP + lane];
+        const int x = x0 + lc;
+        if (x < nx)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int y = y0 + lr + 8 * j;
+                if (y < ny) dst[(size_t)y * nx + x] = so[(lr + 8 * j) * OP + lc];
             }
-        }
     }
 }
 
@@ -651,9 +689,35 @@ DevTaps dev_taps(const of3d_plan* p) {
 unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 template <typename T>
-void launch_k1(dim3 g, size_t lds, hipStream_t s, const Frames& fr, long long fstride, int ny, int nx, int fz0, int zb0,
-               DevTaps tp, double* B, size_t fs, int need_b4) {
-    hipLaunchKernelGGL(k_grad_xy<T>, g, dim3(64, 4), lds, s, fr, fstride, ny, nx, fz0, zb0, tp, B, fs, need_b4);
+const void* k1_kernel(int rd) {
+    const int nj = (K1_TY + 2 * rd + 3) / 4;
+    if (nj <= 8) return (const void*)k_grad_xy<T, 8>;
+    if (nj <= 12) return (const void*)k_grad_xy<T, 12>;
+    return (const void*)k_grad_xy<T, 16>;
+}
+
+const void* k1_kernel_dt(int dtype, int rd) {
+    switch (dtype) {
+        case OF3D_U8: return k1_kernel<uint8_t>(rd);
+        case OF3D_U16: return k1_kernel<uint16_t>(rd);
+        case OF3D_I16: return k1_kernel<int16_t>(rd);
+        case OF3D_U32: return k1_kernel<uint32_t>(rd);
+        case OF3D_I32: return k1_kernel<int32_t>(rd);
+        case OF3D_F32: return k1_kernel<float>(rd);
+        default: return k1_kernel<double>(rd);
+    }
+}
+
+const void* k0_kernel_dt(int dtype) {
+    switch (dtype) {
+        case OF3D_U8: return (const void*)k_tderiv<uint8_t>;
+        case OF3D_U16: return (const void*)k_tderiv<uint16_t>;
+        case OF3D_I16: return (const void*)k_tderiv<int16_t>;
+        case OF3D_U32: return (const void*)k_tderiv<uint32_t>;
+        case OF3D_I32: return (const void*)k_tderiv<int32_t>;
+        case OF3D_F32: return (const void*)k_tderiv<float>;
+        default: return (const void*)k_tderiv<double>;
+    }
 }
 
 // K5 variants: rows of the staged window each thread prefetches into
@@ -670,32 +734,27 @@ const void* k5_kernel(int rw) {
     }
 }
 
+int ring_for(int need) { return need <= 64 ? 64 : 128; }
+
 const void* k3_kernel(int np, int rw) {
-    const int nj = nj_for(K3_YC + 2 * rw);
-#define K3K(NP)                                                       \
-    switch (nj) {                                                     \
-        case 16: return (const void*)k_prod_wy<NP, 16>;               \
-        case 20: return (const void*)k_prod_wy<NP, 20>;               \
-        case 24: return (const void*)k_prod_wy<NP, 24>;               \
-        default: return (const void*)k_prod_wy<NP, 32>;               \
-    }
-    if (np == 9) { K3K(9) } else { K3K(5) }
-#undef K3K
+    const int hr = ring_for(K3_STEP + 2 * rw);
+    if (np == 9) return hr == 64 ? (const void*)k_prod_wy<9, 64> : (const void*)k_prod_wy<9, 128>;
+    return hr == 64 ? (const void*)k_prod_wy<5, 64> : (const void*)k_prod_wy<5, 128>;
 }
 
 const void* k4_kernel(int nf, int rw) {
-    const int nj = (K4_TX + 2 * rw + 63) / 64;
-    if (nf == 9) return nj <= 1 ? (const void*)k_wx<9, 1> : (const void*)k_wx<9, 2>;
-    return nj <= 1 ? (const void*)k_wx<5, 1> : (const void*)k_wx<5, 2>;
+    const int hc = ring_for(K4_TX + 2 * rw);
+    if (nf == 9) return hc == 64 ? (const void*)k_wx<9, 64> : (const void*)k_wx<9, 128>;
+    return hc == 64 ? (const void*)k_wx<5, 64> : (const void*)k_wx<5, 128>;
 }
 
 int set_attrs(of3d_plan* p) {
     if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
-    if (K4_TX + 2 * p->rw > 128) return fail("of3d: wSig too large (window radius > 48)");
+    if (K4_TX + 2 * p->rw > 128 || K3_STEP + 2 * p->rw > 128) return fail("of3d: wSig too large (window radius > 48)");
     p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * sizeof(double);
     p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
-    p->k3_lds = (size_t)(K3_YC + 2 * p->rw) * 64 * sizeof(double);
-    p->k4_lds = (size_t)K4_ROWS * ((K4_TX + 2 * p->rw) | 1) * sizeof(double);
+    p->k3_lds = (size_t)ring_for(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
+    p->k4_lds = (size_t)K4_ROWS * ((ring_for(K4_TX + 2 * p->rw) + 1) + (K4_TX + 1)) * sizeof(double);
     p->k5_lds = (size_t)2 * (K5_ZC + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
@@ -704,10 +763,7 @@ int set_attrs(of3d_plan* p) {
         return 0;
     };
     int rc = 0;
-    rc |= attr((const void*)k_grad_xy<uint8_t>, p->k1_lds) | attr((const void*)k_grad_xy<uint16_t>, p->k1_lds) |
-          attr((const void*)k_grad_xy<int16_t>, p->k1_lds) | attr((const void*)k_grad_xy<uint32_t>, p->k1_lds) |
-          attr((const void*)k_grad_xy<int32_t>, p->k1_lds) | attr((const void*)k_grad_xy<float>, p->k1_lds) |
-          attr((const void*)k_grad_xy<double>, p->k1_lds);
+    for (int dt = OF3D_U8; dt <= OF3D_F64; ++dt) rc |= attr(k1_kernel_dt(dt, p->rd), p->k1_lds);
     rc |= attr((const void*)k_grad_z, p->k2_lds);
     rc |= attr(k3_kernel(9, p->rw), p->k3_lds) | attr(k3_kernel(5, p->rw), p->k3_lds);
     rc |= attr(k4_kernel(9, p->rw), p->k4_lds) | attr(k4_kernel(5, p->rw), p->k4_lds);
@@ -759,7 +815,7 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         if (evs) OF3D_HIP(hipEventRecord(evs[i], s)); \
     } while (0)
     OF3D_MARK(0);
-    // K1 — frames equally spaced (one stack) are addressed by stride
+    // K0 + K1 — frames equally spaced (one stack) are addressed by stride
     {
         const size_t es = dtype_size(dtype);
         long long fstride = 0;
@@ -770,19 +826,25 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
             for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
             if (eq) fstride = d / (long long)es;
         }
-        dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), nb);
-        const int fz0 = (int)frame_z0, zb0 = (int)R.zb0, need_b4 = p->ndim == 3;
-        const size_t L = p->k1_lds;
-        switch (dtype) {
-            case OF3D_U8: launch_k1<uint8_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_U16: launch_k1<uint16_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_I16: launch_k1<int16_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_U32: launch_k1<uint32_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_I32: launch_k1<int32_t>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_F32: launch_k1<float>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
-            case OF3D_F64: launch_k1<double>(g, L, s, fr, fstride, ny, nx, fz0, zb0, tp, p->X, fs, need_b4); break;
+        const size_t plane = (size_t)ny * nx;
+        size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)nb * plane;
+        int rt_arg = p->rt;
+        double* D0 = p->Y;  // Y field 0 is free until K2 writes it
+        {
+            const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
+            void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
+                            (void*)&D0};
+            OF3D_HIP(hipLaunchKernel(k0_kernel_dt(dtype), dim3(blocks), dim3(256), args, 0, s));
         }
-        OF3D_HIP(hipGetLastError());
+        {
+            const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
+            const double* D0c = D0;
+            int need_b4 = p->ndim == 3, nb_arg = nb;
+            dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
+            void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
+                            (void*)&p->X, (void*)&fs, (void*)&need_b4};
+            OF3D_HIP(hipLaunchKernel(k1_kernel_dt(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
+        }
     }
     OF3D_MARK(1);
     const double* G;
@@ -800,19 +862,17 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     double* Q = p->ndim == 3 ? p->Y : p->X;
     const int nf = p->ndim == 3 ? 9 : 5;
     {
-        dim3 g(cdiv(nx, 64), cdiv(ny, K3_YC), cdiv(ng, K3_NZB) * nf);
-        int rw_arg = p->rw, ng_arg = ng;
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&ng_arg, (void*)&fs, (void*)&tp.w,
-                        (void*)&rw_arg};
+        dim3 g(cdiv(nx, 64), 1, ng * nf);
+        int rw_arg = p->rw;
+        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k3_kernel(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
     }
     OF3D_MARK(3);
     {
-        dim3 g(cdiv(nx, K4_TX), cdiv(ny, K4_ROWS), cdiv(ng, K4_NZB) * nf);
-        int rw_arg = p->rw, ng_arg = ng;
+        dim3 g(1, cdiv(ny, K4_ROWS), ng * nf);
+        int rw_arg = p->rw;
         const double* Pc = P;
-        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&ng_arg, (void*)&fs, (void*)&tp.w,
-                        (void*)&rw_arg};
+        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k4_kernel(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
     }
     OF3D_MARK(4);
