@@ -1,0 +1,148 @@
+"""Multi-GPU decomposition of the LK hot path.
+
+Two ways the path shards, both one process per GPU:
+
+1. Frame replicas — output frames are independent (the reference's own note,
+   calc_flow.py:512: "this could become a parfor loop").  Rank r takes output
+   frames r, r+P, ...; no collective on the data path.
+
+2. z-slabs of one large frame — rank p owns output planes [z0_p, z1_p).  Every
+   stage clamps at the GLOBAL volume edge (scipy mode='nearest' on the whole
+   volume), so a slab computed from input planes [z0-H, z1+H) ∩ [0, Nz) with
+   H = rd + rw (gradient z-pass radius + window z-pass radius) is bit-identical
+   to the same planes of the unsharded result.  The plan reports the exact
+   input range (of3d_plan_input_range).  When the input stack is already
+   distributed across GPUs (each rank holds its own planes), the halo planes
+   come from the z-neighbours: ``exchange_halos`` sends/receives them with
+   torch.distributed point-to-point (RCCL over xGMI for CUDA tensors, gloo for
+   CPU tensors) — the only collective on this path.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from .taps import make_taps, radii
+
+
+def frame_assignment(n_frames: int, rank: int, world: int) -> list:
+    """Output frames of rank `rank` under round-robin replicas."""
+    return list(range(rank, n_frames, world))
+
+
+def zslab_bounds(nz: int, rank: int, world: int) -> tuple:
+    """Balanced contiguous output planes [z0, z1) of rank `rank` (may be empty when world > nz)."""
+    base, extra = divmod(nz, world)
+    z0 = rank * base + min(rank, extra)
+    z1 = z0 + base + (1 if rank < extra else 0)
+    return z0, z1
+
+
+def halo_planes(nz: int, z0: int, z1: int, rd: int, rw: int) -> tuple:
+    """Input planes [zi0, zi1) a slab producing outputs [z0, z1) must hold (matches of3d_plan_input_range)."""
+    if z1 <= z0:
+        return z0, z0
+    h = rd + rw
+    return max(z0 - h, 0), min(z1 + h, nz)
+
+
+def exchange_halos(local, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
+    """Assemble the input planes [max(z0-halo,0), min(z1+halo,nz)) of this rank.
+
+    ``local``: tensor (..., z1-z0, Ny, Nx) — this rank's own planes on axis -3
+    (CPU tensors over gloo, CUDA tensors over RCCL).  Neighbour planes are
+    exchanged with batched point-to-point ops; ranks at the global edge get
+    nothing from outside (the kernels clamp there).  Slabs thinner than the
+    halo pull from several ranks.  Returns (tensor, zi0)."""
+    import torch
+    import torch.distributed as dist
+
+    zi0, zi1 = max(z0 - halo, 0), min(z1 + halo, nz)
+    bounds = [zslab_bounds(nz, r, world) for r in range(world)]
+    ops, recv = [], {}
+    for r in range(world):
+        if r == rank:
+            continue
+        rz0, rz1 = bounds[r]
+        # planes rank r needs from me
+        need0, need1 = max(rz0 - halo, 0), min(rz1 + halo, nz)
+        s0, s1 = max(need0, z0), min(need1, z1)
+        if s1 > s0:
+            send = local[..., s0 - z0:s1 - z0, :, :].contiguous()
+            ops.append(dist.P2POp(dist.isend, send, r, group))
+        # planes I need from rank r
+        g0, g1 = max(zi0, rz0), min(zi1, rz1)
+        if g1 > g0:
+            shape = list(local.shape)
+            shape[-3] = g1 - g0
+            buf = torch.empty(shape, dtype=local.dtype, device=local.device)
+            recv[r] = (g0, g1, buf)
+            ops.append(dist.P2POp(dist.irecv, buf, r, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    pieces = []
+    for r in range(world):
+        if r == rank:
+            pieces.append((z0, local))
+        elif r in recv:
+            pieces.append((recv[r][0], recv[r][2]))
+    pieces.sort(key=lambda t: t[0])
+    out = torch.cat([p for _, p in pieces if p.shape[-3] > 0], dim=-3)
+    assert out.shape[-3] == zi1 - zi0
+    return out, zi0
+
+
+class SlabRunner:
+    """Computes the output planes [z0, z1) of a 3D frame on one GPU from device-resident input planes.
+
+    frames: uint16/... device tensor (2*rt+1, zi1-zi0, Ny, Nx) holding planes [zi0, zi1)."""
+
+    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=0, timing=0):
+        self.nz, self.ny, self.nx = nz, ny, nx
+        self.z0, self.z1 = z0, z1
+        self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
+        self.plan = _lib.Plan(3, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=device,
+                              max_out_planes=max(z1 - z0, 1), timing=timing)
+        self.zi0, self.zi1 = self.plan.input_range(z0, z1)
+
+    def run(self, frames, dtype_code, vx, vy, vz, rel, stream=0):
+        ptrs = [frames[i].data_ptr() for i in range(frames.shape[0])]
+        self.plan.execute(ptrs, dtype_code, self.zi0, self.z0, self.z1, vx.data_ptr(), vy.data_ptr(),
+                          vz.data_ptr(), rel.data_ptr(), stream)
+
+    def close(self):
+        self.plan.close()
+
+
+def flow3d_zslabs_host(images, xyzSig, tSig, wSig, world, device=0):
+    """Reference-shaped helper: run calc_flow3D as `world` z-slabs on one device
+    (virtual ranks) through device plans, concatenating the slabs.  Used to
+    prove slab decomposition is bit-identical to the unsharded path."""
+    import torch
+
+    a = np.ascontiguousarray(images)
+    nt, nz, ny, nx = a.shape
+    rd, rs, rt, rw = radii(xyzSig, tSig, wSig)
+    c = nt // 2
+    win = a[c - rt:c + rt + 1]
+    code = _lib.DTYPE_CODES[a.dtype]
+    dev = torch.device("cuda", device)
+    outs = [np.empty((nz, ny, nx)) for _ in range(3)] + [np.empty((nz, ny, nx), np.float32)]
+    for rank in range(world):
+        z0, z1 = zslab_bounds(nz, rank, world)
+        if z1 <= z0:
+            continue
+        sr = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=device)
+        part = np.ascontiguousarray(win[:, sr.zi0:sr.zi1])
+        t_in = torch.from_numpy(part.view(np.int16) if a.dtype == np.uint16 else part).to(dev)
+        n = (z1 - z0) * ny * nx
+        vx, vy, vz = (torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3))
+        rel = torch.empty(n, dtype=torch.float32, device=dev)
+        sr.run(t_in, code, vx, vy, vz, rel, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        for o, t in zip(outs, (vx, vy, vz, rel)):
+            o[z0:z1] = t.cpu().numpy().reshape(z1 - z0, ny, nx)
+        sr.close()
+    return tuple(outs)
