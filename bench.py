@@ -84,15 +84,25 @@ def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane):
     }
 
 
-def load_pmc_traffic(kernel, cfg):
+STAGE_KERNELS = {"grad_xy": ("k_tderiv", "k_grad_xy"), "grad_z": ("k_grad_z",), "prod_wy": ("k_prod_wy",),
+                 "wx": ("k_wx",), "wz_solve": ("k_wz_solve",)}
+
+
+def load_pmc_traffic(stage, cfg):
+    """HBM bytes per launch of the stage's kernels from the committed rocprofv3 PMC summary
+    (profiles/pmc_<cfg>.json: FETCH_SIZE x2 + WRITE_SIZE, calibrated in profiles/pmc_calibration.json)."""
     path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        ks = d.get("kernels", {})
+        vals = [e.get("hbm_bytes_per_launch") for k, e in ks.items() if k.startswith(STAGE_KERNELS[stage])]
+        if not vals or any(v is None for v in vals):
+            return None
+        return round(sum(vals))
+    except (OSError, ValueError, KeyError):
         return None
 
 
