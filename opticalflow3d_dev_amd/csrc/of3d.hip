@@ -183,6 +183,54 @@ __global__ __launch_bounds__(256) void k_tderiv(Frames fr, long long fstride, si
     }
 }
 
+// Vectorised K0 for one stack (frames `fstride` elements apart): each lane
+// handles V consecutive voxels with one 8- or 16-byte load per frame.
+template <typename T>
+struct K0Vec {
+    static constexpr int V = sizeof(T) == 1 ? 8 : (sizeof(T) == 8 ? 2 : 4);
+    static constexpr int B = V * (int)sizeof(T);  // 8 or 16 bytes
+};
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, double (&v)[K0Vec<T>::V]) {
+    constexpr int V = K0Vec<T>::V;
+    T t[V];
+    if constexpr (K0Vec<T>::B == 8) {
+        const unsigned long long raw = *reinterpret_cast<const unsigned long long*>(p);
+        __builtin_memcpy(t, &raw, 8);
+    } else {
+        const uint4 raw = *reinterpret_cast<const uint4*>(p);
+        __builtin_memcpy(t, &raw, 16);
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = (double)t[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_tderiv_vec(const T* __restrict__ f0, long long fstride, size_t ngroups,
+                                                    int rt, const double* __restrict__ ht,
+                                                    double* __restrict__ D0) {
+    constexpr int V = K0Vec<T>::V;
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
+        const T* p = f0 + gi * V;
+        double c[V], a[V], b[V], dt[V];
+        load_vec<T>(p + (long long)rt * fstride, c);
+#pragma unroll
+        for (int i = 0; i < V; ++i) dt[i] = c[i] * ht[0];
+        for (int k = rt; k >= 1; --k) {
+            load_vec<T>(p + (long long)(rt - k) * fstride, a);
+            load_vec<T>(p + (long long)(rt + k) * fstride, b);
+            const double w = ht[k];
+#pragma unroll
+            for (int i = 0; i < V; ++i) dt[i] = dt[i] + (a[i] - b[i]) * w;
+        }
+        double2* d = reinterpret_cast<double2*>(D0 + gi * V);
+#pragma unroll
+        for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K1: y and x passes of the gradient filters (calc_flow.py:279-288, y first):
 //   A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]
@@ -508,13 +556,15 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
 // staged in LDS (double-buffered, next field's loads in flight during this
 // field's pass); each thread keeps its K5_R outputs of all 9 fields in
 // registers for the pointwise solve.
-constexpr int K5_R = 4, K5_ZC = 4 * K5_R;
+constexpr int K5_G = 8;  // 512-thread blocks: 64 lanes x 8 z-groups x R planes (R = 8 for rw <= 16, else 4)
+constexpr int k5_r(int rw) { return rw <= 16 ? 8 : 4; }
 
-template <typename RelT, int NJ>
-__global__ __launch_bounds__(256, 2) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
+template <typename RelT, int NJ, int K5_R>
+__global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
                                                   size_t fs, const double* __restrict__ hw, int rw, int zo0, int nzo,
                                                   double* __restrict__ vx, double* __restrict__ vy,
                                                   double* __restrict__ vz, RelT* __restrict__ rel) {
+    constexpr int K5_ZC = K5_G * K5_R;
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int H = K5_ZC + 2 * rw;
     const int lane = threadIdx.x, g = threadIdx.y;
@@ -528,7 +578,7 @@ __global__ __launch_bounds__(256, 2) void k_wz_solve(const double* __restrict__ 
         const double* q = Q + f * fs + col;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int row = g + 4 * j;
+            const int row = g + K5_G * j;
             if (row < H) rq[j] = q[(size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps];
         }
     };
@@ -539,7 +589,7 @@ __global__ __launch_bounds__(256, 2) void k_wz_solve(const double* __restrict__ 
         double* buf = sm + (f & 1) * H * 64;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-            const int row = g + 4 * j;
+            const int row = g + K5_G * j;
             if (row < H) buf[row * 64 + lane] = rq[j];
         }
         __syncthreads();
@@ -559,7 +609,11 @@ __global__ __launch_bounds__(256, 2) void k_wz_solve(const double* __restrict__ 
         vx[o] = ox;
         vy[o] = oy;
         vz[o] = oz;
+#if defined(OF3D_ABLATE_K5) && OF3D_ABLATE_K5 == 1
+        rel[o] = (RelT)(acc[5][i] + acc[7][i] + acc[8][i] + acc[3][i] + acc[4][i] + acc[6][i]);
+#else
         rel[o] = (RelT)eigmin3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i]);
+#endif
     }
 }
 
@@ -708,6 +762,23 @@ const void* k1_kernel_dt(int dtype, int rd) {
     }
 }
 
+const void* k0v_kernel_dt(int dtype) {
+    switch (dtype) {
+        case OF3D_U8: return (const void*)k_tderiv_vec<uint8_t>;
+        case OF3D_U16: return (const void*)k_tderiv_vec<uint16_t>;
+        case OF3D_I16: return (const void*)k_tderiv_vec<int16_t>;
+        case OF3D_U32: return (const void*)k_tderiv_vec<uint32_t>;
+        case OF3D_I32: return (const void*)k_tderiv_vec<int32_t>;
+        case OF3D_F32: return (const void*)k_tderiv_vec<float>;
+        default: return (const void*)k_tderiv_vec<double>;
+    }
+}
+
+int k0_vec_width(int dtype) {
+    const size_t es = dtype_size(dtype);
+    return es == 1 ? 8 : (es == 8 ? 2 : 4);
+}
+
 const void* k0_kernel_dt(int dtype) {
     switch (dtype) {
         case OF3D_U8: return (const void*)k_tderiv<uint8_t>;
@@ -726,11 +797,13 @@ int nj_for(int h) { return h <= 64 ? 16 : (h <= 80 ? 20 : (h <= 96 ? 24 : 32)); 
 
 template <typename RelT>
 const void* k5_kernel(int rw) {
-    switch (nj_for(K5_ZC + 2 * rw)) {
-        case 16: return (const void*)k_wz_solve<RelT, 16>;
-        case 20: return (const void*)k_wz_solve<RelT, 20>;
-        case 24: return (const void*)k_wz_solve<RelT, 24>;
-        default: return (const void*)k_wz_solve<RelT, 32>;
+    // rows per thread of the staged window: ceil((K5_G * R + 2rw) / K5_G)
+    if (k5_r(rw) == 8) return (const void*)k_wz_solve<RelT, 12, 8>;  // rw <= 16: (64 + 32) / 8
+    const int nj = (K5_G * 4 + 2 * rw + K5_G - 1) / K5_G;
+    switch (nj <= 10 ? 10 : (nj <= 12 ? 12 : 16)) {
+        case 10: return (const void*)k_wz_solve<RelT, 10, 4>;
+        case 12: return (const void*)k_wz_solve<RelT, 12, 4>;
+        default: return (const void*)k_wz_solve<RelT, 16, 4>;
     }
 }
 
@@ -755,7 +828,7 @@ int set_attrs(of3d_plan* p) {
     p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
     p->k3_lds = (size_t)ring_for(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
     p->k4_lds = (size_t)K4_ROWS * ((ring_for(K4_TX + 2 * p->rw) + 1) + (K4_TX + 1)) * sizeof(double);
-    p->k5_lds = (size_t)2 * (K5_ZC + 2 * p->rw) * 64 * sizeof(double);
+    p->k5_lds = (size_t)2 * (K5_G * k5_r(p->rw) + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
     auto attr = [&](const void* k, size_t b) -> int {
@@ -830,7 +903,17 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)nb * plane;
         int rt_arg = p->rt;
         double* D0 = p->Y;  // Y field 0 is free until K2 writes it
-        {
+        const int V = k0_vec_width(dtype);
+        const size_t vb = (size_t)V * es;
+        const bool vec = fstride != 0 && fstride % V == 0 && off0 % V == 0 && n % V == 0 &&
+                         ((uintptr_t)d_frames[0] % vb) == 0;
+        if (vec) {
+            const void* f0 = (const char*)d_frames[0] + off0 * es;
+            size_t ng = n / V;
+            const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
+            void* args[] = {(void*)&f0, (void*)&fstride, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
+            OF3D_HIP(hipLaunchKernel(k0v_kernel_dt(dtype), dim3(blocks), dim3(256), args, 0, s));
+        } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
             void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
                             (void*)&D0};
@@ -877,13 +960,13 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {
-        dim3 g(cdiv(nx, 64), ny, cdiv(no, K5_ZC));
+        dim3 g(cdiv(nx, 64), ny, cdiv(no, K5_G * k5_r(p->rw)));
         int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
         const double* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
         const void* k5 = p->rel64 ? k5_kernel<double>(p->rw) : k5_kernel<float>(p->rw);
-        OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, 4), args, p->k5_lds, s));
+        OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, K5_G), args, p->k5_lds, s));
     } else {
         const int n = ny * nx;
         hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);
