@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void k_tderiv_vec(const T* __restrict__ f0, lo
 constexpr int K1_R = 4, K1_TY = 4 * K1_R, K1_NZB = 4;
 
 template <typename T, int NJ>
-__global__ __launch_bounds__(256) void k_grad_xy(const T* __restrict__ Ic, const double* __restrict__ D0, int ny,
+__global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, const double* __restrict__ D0, int ny,
                                                  int nx, int nzp, DevTaps tp, double* __restrict__ B, size_t fs,
                                                  int need_b4) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
