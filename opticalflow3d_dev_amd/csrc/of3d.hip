@@ -397,16 +397,17 @@ struct ProdTable<5> {
 
 // Streaming form: a block owns one 64-column strip of one plane and one
 // product, and marches down the whole column height K3_STEP rows at a time.
-// Product rows live in an LDS ring of HR rows (power of two >= K3_STEP + 2rw),
-// keyed by y' = y + rw, so every product row is loaded once; the next step's
-// rows are fetched into registers while the current step's pass runs.
+// The LDS window holds rows y' = y0 .. y0 + K3_STEP + 2rw - 1 (y' = y + rw);
+// after each step its last 2rw rows move to the front (so every row is
+// loaded from memory once, and every tap read is a constant LDS offset); the
+// next step's rows are fetched into registers during the current pass.
 constexpr int K3_STEP = K3_YC;
 
-template <int NP, int HR>
+template <int NP, int TJ>  // TJ >= ceil(2rw / 4): window rows each thread carries over
 __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
                                                  int nx, size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    constexpr int NJ = K3_STEP / 4;  // rows per thread per step
+    constexpr int NJ = K3_STEP / 4;  // new rows per thread per step
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
     const int xs = x < nx ? x : nx - 1;
@@ -417,12 +418,12 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;  // b[] = {0,0,0,1,3,2,3,1,3} / {0,0,1,2,1}
     const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
     const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
-    auto prod = [&](int yp) {  // product at ring key y' (clamped row y' - rw)
-        const size_t o = (size_t)clampi(yp - rw, 0, ny - 1) * nx;
-        return ga[o] * gb[o];
-    };
-    // prologue: rows y' in [0, 2rw) directly, rows [2rw, 2rw + STEP) into registers
-    for (int yp = g; yp < 2 * rw; yp += 4) sm[(yp & (HR - 1)) * 64 + lane] = prod(yp);
+    const int h2 = 2 * rw;
+    double* col = sm + lane;
+    for (int b = g; b < h2; b += 4) {  // prologue: y' in [0, 2rw)
+        const size_t o = (size_t)clampi(b - rw, 0, ny - 1) * nx;
+        col[b * 64] = ga[o] * gb[o];
+    }
     double ra[NJ], rb[NJ];
     auto fetch = [&](int yp0) {
 #pragma unroll
@@ -432,16 +433,17 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
             rb[j] = gb[o];
         }
     };
-    fetch(2 * rw);
+    fetch(h2);
     double* o = P + p * fs + pl + x;
+    double tl[TJ];
     for (int y0 = 0; y0 < ny; y0 += K3_STEP) {
-        // rows y' in [y0 + 2rw, y0 + 2rw + STEP) enter the ring
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) sm[((y0 + 2 * rw + g + 4 * j) & (HR - 1)) * 64 + lane] = ra[j] * rb[j];
+        for (int j = 0; j < NJ; ++j) col[(h2 + g + 4 * j) * 64] = ra[j] * rb[j];
         __syncthreads();
-        if (y0 + K3_STEP < ny) fetch(y0 + K3_STEP + 2 * rw);
+        const bool more = y0 + K3_STEP < ny;
+        if (more) fetch(y0 + K3_STEP + h2);
         double out[K3_R];
-        lds_pass<K3_R, false, 1, true>(sm + lane, 64, y0 + rw + g * K3_R, hw, rw, out, HR - 1);
+        lds_pass<K3_R, false>(col, 64, rw + g * K3_R, hw, rw, out);
         if (x < nx) {
 #pragma unroll
             for (int i = 0; i < K3_R; ++i) {
@@ -449,7 +451,15 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
                 if (y < ny) o[(size_t)y * nx] = out[i];
             }
         }
-        __syncthreads();
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                if (g + 4 * j < h2) tl[j] = col[(K3_STEP + g + 4 * j) * 64];
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+                if (g + 4 * j < h2) col[(g + 4 * j) * 64] = tl[j];
+        }
     }
 }
 
@@ -462,16 +472,18 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
 constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64;
 
 // Streaming form: a block owns 64 rows of one plane and one field, and marches
-// along x K4_TX columns at a time; columns live in an LDS ring of HC columns
-// (power of two >= K4_TX + 2rw, keyed by x' = x + rw, odd row pitch HC + 1 so
-// lane = row reads are conflict-free).  Results leave through a transposing
-// LDS tile for coalesced row stores; the next step's columns are fetched into
-// registers during the current pass.
-template <int NF, int HC>
-__global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
+// along x K4_TX columns at a time.  The LDS window holds columns
+// x' = x0 .. x0 + K4_TX + 2rw - 1 (x' = x + rw) of every row (odd pitch so
+// lane = row reads are conflict-free); after each step the last 2rw columns
+// move to the front.  Results leave through a transposing LDS tile for
+// coalesced row stores; the next step's columns are fetched into registers
+// during the current pass.
+template <int NF, int TJ>  // TJ >= ceil(2rw / 32): tail column groups per loader lane
+__global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
                                             size_t fs, const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    constexpr int PP = HC + 1;
+    const int h2 = 2 * rw;
+    const int PP = (K4_TX + h2) | 1;
     constexpr int OP = K4_TX + 1;
     double* so = sm + K4_ROWS * PP;  // output tile [row][K4_TX]
     const int lane = threadIdx.x, g = threadIdx.y;
@@ -482,26 +494,37 @@ __global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double
     double* dst = Q + f * fs + pl;
     // loader mapping: lanes 0..31 / 32..63 -> two rows, 32 consecutive columns
     const int lc = lane & 31, lr = (lane >> 5) + 2 * g;  // rows lr, lr + 8, ..., lr + 56
-    auto colv = [&](int row, int xp) {
-        return src[(size_t)min(y0 + row, ny - 1) * nx + clampi(xp - rw, 0, nx - 1)];
-    };
-    for (int xp = lc; xp < 2 * rw; xp += 32)
-        for (int row = lr; row < K4_ROWS; row += 8) sm[row * PP + (xp & (HC - 1))] = colv(row, xp);
+    const double* rowp[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rowp[j] = src + (size_t)min(y0 + lr + 8 * j, ny - 1) * nx;
+    auto colv = [&](int j, int xp) { return rowp[j][clampi(xp - rw, 0, nx - 1)]; };
+    for (int xp = lc; xp < h2; xp += 32)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + xp] = colv(j, xp);
     double rv[8];
     auto fetch = [&](int xp0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rv[j] = colv(lr + 8 * j, xp0 + lc);
+        for (int j = 0; j < 8; ++j) rv[j] = colv(j, xp0 + lc);
     };
-    fetch(2 * rw);
+    fetch(h2);
+    double tl[TJ][8];
     for (int x0 = 0; x0 < nx; x0 += K4_TX) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + ((x0 + 2 * rw + lc) & (HC - 1))] = rv[j];
+        for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + h2 + lc] = rv[j];
         __syncthreads();
-        if (x0 + K4_TX < nx) fetch(x0 + K4_TX + 2 * rw);
+        const bool more = x0 + K4_TX < nx;
+        if (more) fetch(x0 + K4_TX + h2);
         double out[K4_R];
-        lds_pass<K4_R, false, 1, true>(sm + lane * PP, 1, x0 + rw + g * K4_R, hw, rw, out, HC - 1);
+        lds_pass<K4_R, false>(sm + lane * PP, 1, rw + g * K4_R, hw, rw, out);
 #pragma unroll
         for (int i = 0; i < K4_R; ++i) so[lane * OP + g * K4_R + i] = out[i];
+        if (more) {
+#pragma unroll
+            for (int t = 0; t < TJ; ++t)
+                if (lc + 32 * t < h2)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) tl[t][j] = sm[(lr + 8 * j) * PP + K4_TX + lc + 32 * t];
+        }
         __syncthreads();
         const int x = x0 + lc;
         if (x < nx)
@@ -510,6 +533,13 @@ __global__ __launch_bounds__(256) void k_wx(const double* __restrict__ P, double
                 const int y = y0 + lr + 8 * j;
                 if (y < ny) dst[(size_t)y * nx + x] = so[(lr + 8 * j) * OP + lc];
             }
+        if (more) {
+#pragma unroll
+            for (int t = 0; t < TJ; ++t)
+                if (lc + 32 * t < h2)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + lc + 32 * t] = tl[t][j];
+        }
     }
 }
 
@@ -530,10 +560,27 @@ __device__ __forceinline__ void solve3(double x2, double y2, double z2, double x
     vz = nR * ((xy * yz - y2 * xz) * tx + (xy * xz - x2 * yz) * ty + (x2 * y2 - xy * xy) * tz);
 }
 
+// cos(x) for x in [0, pi/3]: Taylor series to x^18 (truncation < 1e-18),
+// Horner with explicit FMAs (the eigen-solve is not bit-matched, see below).
+__device__ __forceinline__ double cos_small(double x) {
+    const double y = x * x;
+    double c = 1.0 / 6402373705728000.0;             // 1/18!
+    c = __builtin_fma(c, -y, 1.0 / 20922789888000.0);  // 1/16!
+    c = __builtin_fma(c, -y, 1.0 / 87178291200.0);     // 1/14!
+    c = __builtin_fma(c, -y, 1.0 / 479001600.0);       // 1/12!
+    c = __builtin_fma(c, -y, 1.0 / 3628800.0);         // 1/10!
+    c = __builtin_fma(c, -y, 1.0 / 40320.0);           // 1/8!
+    c = __builtin_fma(c, -y, 1.0 / 720.0);             // 1/6!
+    c = __builtin_fma(c, -y, 1.0 / 24.0);              // 1/4!
+    c = __builtin_fma(c, -y, 0.5);                     // 1/2!
+    return __builtin_fma(c, -y, 1.0);
+}
+
 // Smallest eigenvalue of the symmetric 3x3 [[a d e][d b f][e f c]] in fp64
 // (trigonometric closed form).  The reference gets it from LAPACK cgeev in
 // complex64 (calc_flow.py:355-357); fp64 here, stored as float32 like the
-// reference's output.
+// reference's output (or kept fp64 with OF3D_REL_F64).
+// lambda_min = q + 2p cos(phi + 2pi/3) = q - 2p cos(pi/3 - phi), phi = acos(r)/3 in [0, pi/3].
 __device__ __forceinline__ double eigmin3(double a, double b, double c, double d, double e, double f) {
     const double p1 = d * d + e * e + f * f;
     if (p1 == 0.0) return fmin(a, fmin(b, c));
@@ -548,7 +595,7 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     double r = 0.5 * detB;
     r = fmin(1.0, fmax(-1.0, r));
     const double phi = acos(r) / 3.0;
-    return q + 2.0 * p * cos(phi + 2.0943951023931957);  // + 2*pi/3
+    return q - 2.0 * p * cos_small(1.0471975511965976 - phi);  // pi/3 - phi
 }
 
 // K5: W z pass + solve + reliability.  Block = 64 x-columns of one row and
@@ -807,27 +854,31 @@ const void* k5_kernel(int rw) {
     }
 }
 
-int ring_for(int need) { return need <= 64 ? 64 : 128; }
-
 const void* k3_kernel(int np, int rw) {
-    const int hr = ring_for(K3_STEP + 2 * rw);
-    if (np == 9) return hr == 64 ? (const void*)k_prod_wy<9, 64> : (const void*)k_prod_wy<9, 128>;
-    return hr == 64 ? (const void*)k_prod_wy<5, 64> : (const void*)k_prod_wy<5, 128>;
+    const int tj = (2 * rw + 3) / 4;  // <= 24 for rw <= 48
+    if (np == 9) {
+        if (tj <= 8) return (const void*)k_prod_wy<9, 8>;
+        if (tj <= 12) return (const void*)k_prod_wy<9, 12>;
+        return (const void*)k_prod_wy<9, 24>;
+    }
+    if (tj <= 8) return (const void*)k_prod_wy<5, 8>;
+    if (tj <= 12) return (const void*)k_prod_wy<5, 12>;
+    return (const void*)k_prod_wy<5, 24>;
 }
 
 const void* k4_kernel(int nf, int rw) {
-    const int hc = ring_for(K4_TX + 2 * rw);
-    if (nf == 9) return hc == 64 ? (const void*)k_wx<9, 64> : (const void*)k_wx<9, 128>;
-    return hc == 64 ? (const void*)k_wx<5, 64> : (const void*)k_wx<5, 128>;
+    const int tj = (2 * rw + 31) / 32;  // <= 3 for rw <= 48
+    if (nf == 9) return tj <= 1 ? (const void*)k_wx<9, 1> : (tj == 2 ? (const void*)k_wx<9, 2> : (const void*)k_wx<9, 3>);
+    return tj <= 1 ? (const void*)k_wx<5, 1> : (tj == 2 ? (const void*)k_wx<5, 2> : (const void*)k_wx<5, 3>);
 }
 
 int set_attrs(of3d_plan* p) {
     if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
-    if (K4_TX + 2 * p->rw > 128 || K3_STEP + 2 * p->rw > 128) return fail("of3d: wSig too large (window radius > 48)");
+
     p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * sizeof(double);
     p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
-    p->k3_lds = (size_t)ring_for(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
-    p->k4_lds = (size_t)K4_ROWS * ((ring_for(K4_TX + 2 * p->rw) + 1) + (K4_TX + 1)) * sizeof(double);
+    p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
+    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * p->rw) | 1) + (K4_TX + 1)) * sizeof(double);
     p->k5_lds = (size_t)2 * (K5_G * k5_r(p->rw) + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
