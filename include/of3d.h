@@ -144,6 +144,23 @@ int of3d_plan_set_timing(of3d_plan* plan, int slots);
 int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
 const char* of3d_stage_name(int i);
 
+/* Copy `bytes` from src to dst on `stream` with a kernel of at most
+ * `max_blocks` workgroups (0 = 64).  Either side may be pinned host memory
+ * (hipHostMalloc / torch pin_memory): used to download a frame's outputs
+ * over PCIe while the next frame's kernels keep the rest of the GPU (the
+ * runtime's own device->host copy runs as a full-GPU blit kernel).
+ * No reference counterpart: process_flow's per-frame output transfer
+ * (calc_flow.py:526-529 writes host arrays). */
+int of3d_copy_async(void* dst, const void* src, size_t bytes, int max_blocks, void* stream);
+
+/* Blocking copy of n buffers on the GPU's DMA (SDMA) engines through the HSA
+ * runtime: no compute units and no HIP stream involved, so a download does
+ * not contend with kernels for the memory pipeline.  Host buffers must be
+ * pinned.  The caller orders it after the producing work (e.g. a download
+ * thread after hipEventSynchronize).  Releases no locks of its own; safe to
+ * call from several threads. */
+int of3d_dma_copy(void* const* dst, const void* const* src, const size_t* bytes, int n);
+
 #ifdef __cplusplus
 }
 #endif

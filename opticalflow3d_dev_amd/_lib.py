@@ -35,6 +35,7 @@ EXPORTED = (
     "of3d_version", "of3d_last_error", "of3d_device_count", "of3d_flow3d", "of3d_flow2d",
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
+    "of3d_copy_async", "of3d_dma_copy",
 )
 
 
@@ -71,6 +72,13 @@ def load():
             raise ImportError(
                 f"opticalflow3d_dev_amd: HIP library not built ({LIB_PATH} missing); "
                 "run `make -C opticalflow3d_dev_amd/csrc` or __graft_entry__.build()")
+        # One HIP runtime per process: torch bundles its own libamdhip64.so.7.
+        # Loaded first, it satisfies our NEEDED entry by soname; loaded after
+        # /opt/rocm's copy, it would start a second runtime that sees no GPUs.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(LIB_PATH)
         P = ctypes.c_void_p
         D = ctypes.POINTER(ctypes.c_double)
@@ -102,6 +110,11 @@ def load():
         lib.of3d_stage_name.restype = ctypes.c_char_p
         lib.of3d_plan_set_timing.argtypes = [P, ctypes.c_int]
         lib.of3d_plan_set_timing.restype = ctypes.c_int
+        lib.of3d_copy_async.argtypes = [P, P, ctypes.c_size_t, ctypes.c_int, P]
+        lib.of3d_copy_async.restype = ctypes.c_int
+        lib.of3d_dma_copy.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.c_int]
+        lib.of3d_dma_copy.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -114,6 +127,18 @@ def check(rc: int) -> int:
     if rc < 0:
         raise RuntimeError("of3d: " + last_error())
     return rc
+
+
+def copy_async(dst_ptr, src_ptr, nbytes, max_blocks=0, stream=0):
+    """of3d_copy_async: kernel copy with at most max_blocks workgroups (pinned host <-> device)."""
+    check(load().of3d_copy_async(dst_ptr, src_ptr, nbytes, max_blocks, stream))
+
+
+def dma_copy(dst_ptrs, src_ptrs, nbytes):
+    """of3d_dma_copy: blocking SDMA copies (pinned host / device buffers); ctypes drops the GIL."""
+    n = len(dst_ptrs)
+    check(load().of3d_dma_copy((ctypes.c_void_p * n)(*dst_ptrs), (ctypes.c_void_p * n)(*src_ptrs),
+                               (ctypes.c_size_t * n)(*nbytes), n))
 
 
 def device_index() -> int:

@@ -209,26 +209,87 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
 
     if fileType == 'OneTif':
         allImages = tf.memmap(imDir / (imName + '.tif'))
-        load = lambda hh: allImages[hh:hh + NtChunk]
+        load_frame = lambda i: allImages[i]
     else:
-        load = lambda hh: np.stack([tf.imread(imDir / fileList[hh + jj]) for jj in range(NtChunk)])
-    for hh in range(0, int(Nt) - NtChunk + 1):
-        loopStart = datetime.now()
-        print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
-        images = load(hh)
-        out = flow(images, xyzSig, tSig, wSig)
-        tstr = str(hh + NtSlice).zfill(4)
-        for n, arr in zip(names, out):
-            tf.imwrite(prefix + '_' + n + '_t' + tstr + '.tiff', arr, photometric='minisblack')
-        del out, images
-        framestime = datetime.now()
-        print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(framestime - loopStart))
+        load_frame = lambda i: tf.imread(imDir / fileList[i])
+    nOut = int(Nt) - NtChunk + 1
+    rt = math.ceil(3 * tSig)
+    if nOut > 0 and NtChunk == 2 * rt + 1:
+        _process_stream(load_frame, nOut, NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix, names)
+    else:  # window and temporal taps disagree (non-integer 6*tSig+1): one upload per window
+        for hh in range(0, nOut):
+            loopStart = datetime.now()
+            print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
+            images = np.stack([load_frame(hh + jj) for jj in range(NtChunk)])
+            out = flow(images, xyzSig, tSig, wSig)
+            _write_frame(prefix, names, hh + NtSlice, out)
+            del out, images
+            print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(datetime.now() - loopStart))
 
     for hh in range(int(Nt) - NtSlice, int(Nt)):
         print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
 
 
 calc_flow = process_flow
+
+
+def _write_frame(prefix, names, frame, out, pool=None):
+    """The reference's per-frame outputs (calc_flow.py:526-529 / :579-581);
+    with a thread pool the files are written concurrently."""
+    tstr = str(frame).zfill(4)
+    paths = [prefix + '_' + n + '_t' + tstr + '.tiff' for n in names]
+    if pool is None:
+        for path, arr in zip(paths, out):
+            tf.imwrite(path, arr, photometric='minisblack')
+    else:
+        for f in [pool.submit(tf.imwrite, path, arr, photometric='minisblack') for path, arr in zip(paths, out)]:
+            f.result()
+
+
+class _Shape:
+    def __init__(self, shape):
+        self.shape = shape
+
+
+def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names):
+    """process_flow's loop on a device-resident frame ring (stream.py): one
+    frame read + upload per output frame; compute, download and TIFF writing
+    of consecutive frames overlap.  Files and stdout lines are the reference's
+    (both lines of a frame are printed once its files are written)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from .stream import FlowStream, Writer
+
+    first = np.asarray(load_frame(0))
+    if len((NtChunk,) + first.shape) != ndim + 1:
+        print(_now() + ' - Processing frame ' + str(NtSlice) + '...')
+        _check_args(_Shape((NtChunk,) + first.shape), ndim + 1, tSig, MSG_NDIM_3D if ndim == 3 else MSG_NDIM_2D)
+    dt = first.dtype.newbyteorder('=') if first.dtype.byteorder not in ('=', '|') else first.dtype
+    fs = FlowStream(ndim, first.shape, dt, xyzSig, tSig, wSig)
+
+    def finish(frame, start, start_str, pending):
+        print(start_str + ' - Processing frame ' + str(frame) + '...')
+        try:
+            _write_frame(prefix, names, frame, pending.result(), pool)
+        finally:
+            pending.release()
+        print(_now() + ' - Frame ' + str(frame) + ' saved.  Duration: ' + str(datetime.now() - start))
+
+    pool = ThreadPoolExecutor(len(names))
+    writer = Writer(finish)
+    try:
+        fs.push(first)
+        for i in range(1, NtChunk - 1):
+            fs.push(load_frame(i))
+        for hh in range(nOut):
+            start = datetime.now()
+            start_str = str(start)
+            fs.push(load_frame(hh + NtChunk - 1))
+            writer.put(hh + NtSlice, start, start_str, fs.submit())
+    finally:
+        writer.close()
+        pool.shutdown()
+        fs.close()
 
 
 def _fmt_csv(v):

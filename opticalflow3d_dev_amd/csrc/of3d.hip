@@ -20,6 +20,8 @@
 // (mode='nearest'); products and the solve copy calc_flow.py's expression
 // trees.  Built with -ffp-contract=off (no FMA) and IEEE div/sqrt.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -183,8 +185,9 @@ __global__ __launch_bounds__(256) void k_tderiv(Frames fr, long long fstride, si
     }
 }
 
-// Vectorised K0 for one stack (frames `fstride` elements apart): each lane
-// handles V consecutive voxels with one 8- or 16-byte load per frame.
+// Vectorised K0 (any frame order, e.g. a device ring buffer; every frame
+// aligned to the vector width): each lane handles V consecutive voxels with
+// one 8- or 16-byte load per frame.
 template <typename T>
 struct K0Vec {
     static constexpr int V = sizeof(T) == 1 ? 8 : (sizeof(T) == 8 ? 2 : 4);
@@ -207,20 +210,19 @@ __device__ __forceinline__ void load_vec(const T* p, double (&v)[K0Vec<T>::V]) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_tderiv_vec(const T* __restrict__ f0, long long fstride, size_t ngroups,
-                                                    int rt, const double* __restrict__ ht,
-                                                    double* __restrict__ D0) {
+__global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size_t ngroups, int rt,
+                                                    const double* __restrict__ ht, double* __restrict__ D0) {
     constexpr int V = K0Vec<T>::V;
     const size_t st = (size_t)gridDim.x * 256;
     for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
-        const T* p = f0 + gi * V;
+        const size_t o = off0 + gi * V;
         double c[V], a[V], b[V], dt[V];
-        load_vec<T>(p + (long long)rt * fstride, c);
+        load_vec<T>(reinterpret_cast<const T*>(fr.p[rt]) + o, c);
 #pragma unroll
         for (int i = 0; i < V; ++i) dt[i] = c[i] * ht[0];
         for (int k = rt; k >= 1; --k) {
-            load_vec<T>(p + (long long)(rt - k) * fstride, a);
-            load_vec<T>(p + (long long)(rt + k) * fstride, b);
+            load_vec<T>(reinterpret_cast<const T*>(fr.p[rt - k]) + o, a);
+            load_vec<T>(reinterpret_cast<const T*>(fr.p[rt + k]) + o, b);
             const double w = ht[k];
 #pragma unroll
             for (int i = 0; i < V; ++i) dt[i] = dt[i] + (a[i] - b[i]) * w;
@@ -381,19 +383,6 @@ __global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, in
 // pass), then each thread produces K3_R rows by a register-rotated window.
 // ---------------------------------------------------------------------------
 constexpr int K3_R = 8, K3_YC = 4 * K3_R;
-
-template <int NP>
-struct ProdTable;
-template <>
-struct ProdTable<9> {
-    static constexpr int a[9] = {2, 1, 3, 2, 2, 2, 1, 1, 3};
-    static constexpr int b[9] = {0, 0, 0, 1, 3, 2, 3, 1, 3};
-};
-template <>
-struct ProdTable<5> {
-    static constexpr int a[5] = {2, 1, 2, 2, 1};
-    static constexpr int b[5] = {0, 0, 1, 2, 1};
-};
 
 // Streaming form: a block owns one 64-column strip of one plane and one
 // product, and marches down the whole column height K3_STEP rows at a time.
@@ -956,13 +945,12 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         double* D0 = p->Y;  // Y field 0 is free until K2 writes it
         const int V = k0_vec_width(dtype);
         const size_t vb = (size_t)V * es;
-        const bool vec = fstride != 0 && fstride % V == 0 && off0 % V == 0 && n % V == 0 &&
-                         ((uintptr_t)d_frames[0] % vb) == 0;
+        bool vec = off0 % V == 0 && n % V == 0;
+        for (int i = 0; vec && i < nwin; ++i) vec = ((uintptr_t)d_frames[i] % vb) == 0;
         if (vec) {
-            const void* f0 = (const char*)d_frames[0] + off0 * es;
             size_t ng = n / V;
             const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
-            void* args[] = {(void*)&f0, (void*)&fstride, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
+            void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
             OF3D_HIP(hipLaunchKernel(k0v_kernel_dt(dtype), dim3(blocks), dim3(256), args, 0, s));
         } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
@@ -1207,6 +1195,30 @@ int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, i
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// Bounded-footprint copy (of3d_copy_async): 16-byte lanes, non-temporal
+// stores, grid-stride over at most max_blocks workgroups; byte tail by block 0.
+// ---------------------------------------------------------------------------
+namespace {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n16,
+                                              const unsigned char* __restrict__ tsrc, unsigned char* __restrict__ tdst,
+                                              int tail) {
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += st)
+        __builtin_nontemporal_store(src[i], &dst[i]);
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail) tdst[threadIdx.x] = tsrc[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_copy_bytes(const unsigned char* __restrict__ src,
+                                                    unsigned char* __restrict__ dst, size_t n) {
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) dst[i] = src[i];
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
 // C-ABI
 // ---------------------------------------------------------------------------
 extern "C" {
@@ -1295,5 +1307,65 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
 }
 
 const char* of3d_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
+
+int of3d_dma_copy(void* const* dst, const void* const* src, const size_t* bytes, int n) {
+    if (n <= 0) return 0;
+    if (!dst || !src || !bytes) return fail("of3d: null argument");
+    static std::once_flag once;
+    static hsa_status_t init = HSA_STATUS_ERROR;
+    std::call_once(once, [] { init = hsa_init(); });  // reference-counted; the HIP runtime holds one too
+    if (init != HSA_STATUS_SUCCESS) return fail("of3d: hsa_init failed");
+    hsa_signal_t sig;
+    if (hsa_signal_create(n, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return fail("of3d: hsa_signal_create failed");
+    int issued = 0;
+    std::string err;
+    for (; issued < n; ++issued) {
+        const int i = issued;
+        if (bytes[i] == 0) {
+            hsa_signal_subtract_relaxed(sig, 1);
+            continue;
+        }
+        hsa_amd_pointer_info_t si{}, di{};
+        si.size = sizeof(si);
+        di.size = sizeof(di);
+        if (hsa_amd_pointer_info(src[i], &si, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+            hsa_amd_pointer_info(dst[i], &di, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+            si.type == HSA_EXT_POINTER_TYPE_UNKNOWN || di.type == HSA_EXT_POINTER_TYPE_UNKNOWN) {
+            err = "of3d: dma copy needs device or pinned host buffers";
+            break;
+        }
+        if (hsa_amd_memory_async_copy(dst[i], di.agentOwner, src[i], si.agentOwner, bytes[i], 0, nullptr, sig) !=
+            HSA_STATUS_SUCCESS) {
+            err = "of3d: hsa_amd_memory_async_copy failed";
+            break;
+        }
+    }
+    if (issued < n) hsa_signal_subtract_relaxed(sig, n - issued);  // drop the copies never issued
+    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
+    hsa_signal_destroy(sig);
+    if (!err.empty()) return fail(err.c_str());
+    return 0;
+}
+
+int of3d_copy_async(void* dst, const void* src, size_t bytes, int max_blocks, void* stream) {
+    if (bytes == 0) return 0;
+    if (!dst || !src) return fail("of3d: null argument");
+    if (max_blocks < 0) return fail("of3d: max_blocks must be >= 0");
+    const unsigned mb = max_blocks ? (unsigned)max_blocks : 64u;
+    hipStream_t s = (hipStream_t)stream;
+    if ((uintptr_t)dst % 16 == 0 && (uintptr_t)src % 16 == 0) {
+        const size_t n16 = bytes / 16;
+        const int tail = (int)(bytes % 16);
+        const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(mb, (n16 + 255) / 256));
+        hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, (const u32x4*)src, (u32x4*)dst, n16,
+                           (const unsigned char*)src + n16 * 16, (unsigned char*)dst + n16 * 16, tail);
+    } else {
+        const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(mb, (bytes + 255) / 256));
+        hipLaunchKernelGGL(k_copy_bytes, dim3(blocks), dim3(256), 0, s, (const unsigned char*)src,
+                           (unsigned char*)dst, bytes);
+    }
+    OF3D_HIP(hipGetLastError());
+    return 0;
+}
 
 }  // extern "C"

@@ -1,0 +1,261 @@
+"""Streaming driver for time series.
+
+The reference's process_flow loads all NtChunk = 6*tSig+1 frames of every
+window for every output frame (calc_flow.py:518, :571-574), computes, then
+writes four TIFFs synchronously (:526-529).  Here:
+
+* the input frames live in a device ring of 2*rt+1 slots: each output frame
+  costs ONE host->device frame upload (the plan takes a table of frame
+  pointers, so the ring is never shifted);
+* uploads, compute and downloads run on their own HIP streams, ordered by
+  events (upload of frame t+1 overlaps compute of frame t);
+* outputs land in pinned host buffers and are handed to a writer thread, so
+  TIFF writing overlaps the next frames' transfer and compute.
+
+Results are the same kernels as calc_flow3D/calc_flow2D (bit-identical).
+"""
+
+from __future__ import annotations
+
+import queue
+import threading
+import time
+
+import numpy as np
+
+from . import _lib
+from .taps import make_taps, radii
+
+# torch storage type holding each kernel-native input dtype (same width; the kernels read the bits)
+_TORCH_VIEW = {
+    np.dtype(np.uint8): "uint8",
+    np.dtype(np.uint16): "int16",
+    np.dtype(np.int16): "int16",
+    np.dtype(np.uint32): "int32",
+    np.dtype(np.int32): "int32",
+    np.dtype(np.float32): "float32",
+    np.dtype(np.float64): "float64",
+}
+
+
+class FlowStream:
+    """Device-resident sliding window over a frame sequence.
+
+    push(frame) uploads one frame (shape vol_shape); once 2*rt+1 frames are
+    resident, submit() computes the flow of the window's centre frame and
+    returns a Pending whose .result() gives host arrays (vx, vy, [vz,] rel);
+    .release() hands the buffer set back (at most `depth` frames in flight)."""
+
+    def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
+                 d2h_blocks=64):
+        import torch
+
+        self.torch = torch
+        self.ndim = ndim
+        self.device = _lib.device_index() if device is None else device
+        self.dev = torch.device("cuda", self.device)
+        dt = np.dtype(dtype)
+        if dt not in _TORCH_VIEW:
+            dt = np.dtype(np.float64)
+        self.np_dtype = dt
+        self.code = _lib.DTYPE_CODES[dt]
+        tdt = getattr(torch, _TORCH_VIEW[dt])
+        if ndim == 3:
+            nz, ny, nx = vol_shape
+        else:
+            (ny, nx), nz = vol_shape, 1
+        self.shape = tuple(vol_shape)
+        self.nvox = nz * ny * nx
+        self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
+        self.nwin = 2 * self.rt + 1
+        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device)
+        self.ring = torch.empty((self.nwin, self.nvox), dtype=tdt, device=self.dev)
+        self.order = []  # ring slots of the resident frames, oldest first
+        self.free = list(range(self.nwin))
+        self.stage = [torch.empty(self.nvox, dtype=tdt).pin_memory() for _ in range(2)]
+        self.stage_np = [t.numpy().view(dt).reshape(self.shape) for t in self.stage]
+        self.stage_evt = [None, None]
+        self.stage_i = 0
+        # Downloads (d2h):
+        #   "dma"     of3d_dma_copy on the SDMA engines from a download thread
+        #             once the frame's kernels are done: no CU time, and the
+        #             next frame's kernels run at full speed meanwhile;
+        #   "kernel"  of3d_copy_async, d2h_blocks workgroups on a stream of its
+        #             own priority (hence its own hardware queue);
+        #   "runtime" torch copy_ — HIP's device->host path is a blit kernel
+        #             over the whole GPU.
+        # Kernel-driven PCIe writes (the last two) back up the memory pipeline
+        # shared with the compute kernels and slow them several-fold.
+        if d2h not in ("dma", "kernel", "runtime"):
+            raise ValueError("d2h must be 'dma', 'kernel' or 'runtime'")
+        self.d2h_mode = d2h
+        self.h2d = torch.cuda.Stream(device=self.dev)
+        self.comp = torch.cuda.Stream(device=self.dev)
+        self.d2h = torch.cuda.Stream(device=self.dev, priority=-1)
+        self.dl_q = None
+        self.stats = {"dl_wait_s": 0.0, "dl_copy_s": 0.0, "dl_n": 0}
+        self.trace = None  # list -> (time, event) records of the download thread
+        if d2h == "dma":
+            self.dl_q = queue.Queue()
+            self.dl_thread = threading.Thread(target=self._download_loop, daemon=True)
+            self.dl_thread.start()
+        nout = 4 if ndim == 3 else 3
+        rel_t = torch.float32 if ndim == 3 else torch.float64
+        self.depth = depth
+        self.d2h_blocks = d2h_blocks
+        mk = lambda pin: [torch.empty(self.nvox, dtype=torch.float64, device=None if pin else self.dev,
+                                      pin_memory=pin) for _ in range(nout - 1)] + \
+                         [torch.empty(self.nvox, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
+        self.dout = [mk(False) for _ in range(depth)]
+        self.hout = [mk(True) for _ in range(depth)]
+        self.host_free = [threading.Event() for _ in range(depth)]  # set: writer released the set
+        for e in self.host_free:
+            e.set()
+        self.slot_evt = {}               # ring slot -> event of the last compute that read it
+        self.k = 0
+
+    def push(self, frame):
+        torch = self.torch
+        frame = np.asarray(frame)
+        if frame.shape != self.shape:
+            raise ValueError(f"frame shape {frame.shape} != stream shape {self.shape}")
+        if len(self.order) == self.nwin:  # recycle the oldest slot
+            self.free.append(self.order.pop(0))
+        slot = self.free.pop(0)
+        st = self.stage[self.stage_i]
+        if self.stage_evt[self.stage_i] is not None:
+            self.stage_evt[self.stage_i].synchronize()  # pinned staging buffer free again
+        # one host pass: (byte-swap / astype(float64) as _device_array) into pinned memory
+        np.copyto(self.stage_np[self.stage_i], frame, casting="unsafe")
+        with torch.cuda.stream(self.h2d):
+            if slot in self.slot_evt:
+                self.h2d.wait_event(self.slot_evt[slot])  # no compute still reads this slot
+            self.ring[slot].copy_(st, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.h2d)
+        self.stage_evt[self.stage_i] = ev
+        self.stage_i ^= 1
+        self.order.append(slot)
+
+    @property
+    def ready(self):
+        return len(self.order) == self.nwin
+
+    def submit(self):
+        torch = self.torch
+        assert self.ready
+        b = self.k % self.depth
+        self.k += 1
+        self.host_free[b].wait()  # previous user of this set has released its host buffers,
+        self.host_free[b].clear()  # which also means its D2H (and so its compute) finished
+        dout, hout = self.dout[b], self.hout[b]
+        self.comp.wait_stream(self.h2d)
+        ptrs = [self.ring[s].data_ptr() for s in self.order]
+        vz = dout[2].data_ptr() if self.ndim == 3 else 0
+        self.plan.execute(ptrs, self.code, 0, 0, self.shape[0] if self.ndim == 3 else 1,
+                          dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
+        cev = torch.cuda.Event()
+        cev.record(self.comp)
+        for s in self.order:
+            self.slot_evt[s] = cev
+        pending = Pending(self, b)
+        if self.d2h_mode == "dma":
+            self.dl_q.put((cev, hout, dout, pending))
+            return pending
+        with torch.cuda.stream(self.d2h):
+            self.d2h.wait_event(cev)
+            for h, d in zip(hout, dout):
+                if self.d2h_mode == "kernel":
+                    _lib.copy_async(h.data_ptr(), d.data_ptr(), d.numel() * d.element_size(), self.d2h_blocks,
+                                    self.d2h.cuda_stream)
+                else:
+                    h.copy_(d, non_blocking=True)
+            pending.event = torch.cuda.Event()
+            pending.event.record(self.d2h)
+        return pending
+
+    def _download_loop(self):
+        while True:
+            job = self.dl_q.get()
+            if job is None:
+                return
+            cev, hout, dout, pending = job
+            try:
+                t0 = time.perf_counter()
+                cev.synchronize()
+                t1 = time.perf_counter()
+                _lib.dma_copy([h.data_ptr() for h in hout], [d.data_ptr() for d in dout],
+                              [d.numel() * d.element_size() for d in dout])
+                t2 = time.perf_counter()
+                self.stats["dl_wait_s"] += t1 - t0
+                self.stats["dl_copy_s"] += t2 - t1
+                self.stats["dl_n"] += 1
+                if self.trace is not None:
+                    self.trace += [(t0, "dl_get"), (t1, "dl_cev"), (t2, "dl_done")]
+            except BaseException as e:  # re-raised by Pending.result()
+                pending.error = e
+            pending.done.set()
+
+    def close(self):
+        if self.dl_q is not None:
+            self.dl_q.put(None)
+            self.dl_thread.join()
+            self.dl_q = None
+        self.torch.cuda.synchronize(self.dev)
+        self.plan.close()
+
+
+class Pending:
+    def __init__(self, fs, b):
+        self.fs, self.b = fs, b
+        self.event = None               # D2H on a stream: completion event
+        self.done = threading.Event()   # D2H by the download thread
+        self.error = None
+
+    def result(self):
+        """Host arrays: views of pinned buffers, valid until release()."""
+        if self.event is not None:
+            self.event.synchronize()
+        else:
+            self.done.wait()
+            if self.error is not None:
+                raise self.error
+        shp = self.fs.shape
+        return [t.numpy().reshape(shp) for t in self.fs.hout[self.b]]
+
+    def release(self):
+        self.fs.host_free[self.b].set()
+
+
+class Writer:
+    """Background TIFF writer; jobs run in submission order."""
+
+    def __init__(self, write_fn):
+        self.q = queue.Queue(maxsize=4)
+        self.write_fn = write_fn
+        self.err = None
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job = self.q.get()
+            if job is None:
+                return
+            try:
+                self.write_fn(*job)
+            except BaseException as e:  # surfaced on close()
+                self.err = e
+            finally:
+                self.q.task_done()
+
+    def put(self, *job):
+        if self.err:
+            raise self.err
+        self.q.put(job)
+
+    def close(self):
+        self.q.put(None)
+        self.t.join()
+        if self.err:
+            raise self.err

@@ -327,24 +327,26 @@ def imwrite(path, data, photometric="minisblack", description=None, imagej=False
     data_pos = ifd0_pos + len(blk0)
     data_pos += (-data_pos) % 16
     flat = arr.reshape(-1)
+    body0, blk0 = ifd_block(0, ifd0_pos, data_pos)
+    head = bytearray(header + blk0)
+    head += b"\0" * (data_pos - len(head))
+    # IFDs of pages 1.. assembled in memory (next-IFD links patched there), one write
+    tail = bytearray()
+    base = data_pos + flat.nbytes
+    prev = (head, ifd0_pos + len(body0))  # (buffer, offset of the next-IFD field in it)
+    for i in range(1, npages):
+        if (base + len(tail)) & 1:
+            tail += b"\0"
+        pos = base + len(tail)
+        body, blk = ifd_block(i, pos, data_pos + i * plane_bytes)
+        buf, at = prev
+        buf[at:at + osz] = struct.pack("<" + ofmt, pos)
+        prev = (tail, len(tail) + len(body))
+        tail += blk
     with open(path, "wb") as f:
-        f.write(header)
-        body0, blk0 = ifd_block(0, ifd0_pos, data_pos)
-        f.write(blk0)
-        f.write(b"\0" * (data_pos - f.tell()))
-        f.write(flat.tobytes())
-        prev_next = ifd0_pos + len(body0)
-        for i in range(1, npages):
-            pos = f.tell()
-            pos += pos & 1
-            f.write(b"\0" * (pos - f.tell()))
-            body, blk = ifd_block(i, pos, data_pos + i * plane_bytes)
-            f.write(blk)
-            end = f.tell()
-            f.seek(prev_next)
-            f.write(struct.pack("<" + ofmt, pos))
-            f.seek(end)
-            prev_next = pos + len(body)
+        f.write(head)
+        f.write(memoryview(flat).cast("B"))
+        f.write(tail)
 
 
 def imagej_description(shape, frames=None, slices=None):

@@ -62,3 +62,84 @@ def test_sequencet_3d_natural_order(tmp_path):
     out = tmp_path / "OpticalFlow3D" / "v_t"
     ref = cpu_ref.calc_flow3D(stack, 1, 1, 2, backend="scipy")
     assert bits_equal(tf.imread(out / "v_t_vx_t0003.tiff"), ref[0])
+
+
+def test_stdout_order(tmp_path, capsys):
+    stack = _stack((10, 4, 16, 18), 4)
+    tf.imwrite(tmp_path / "s.tif", stack, imagej=True)
+    process_flow(str(tmp_path), "s", "OneTif", 3, 1, 1, 2)
+    lines = [l.split(" - ", 1)[1] for l in capsys.readouterr().out.splitlines() if " - " in l]
+    want = [f"No data will be saved for frame {h} to avoid edge effects" for h in range(3)]
+    for f in range(3, 7):
+        want += [f"Processing frame {f}...", f"Frame {f} saved."]
+    want += [f"No data will be saved for frame {h} to avoid edge effects" for h in range(7, 10)]
+    assert [l.split("  Duration")[0] for l in lines] == want
+
+
+@pytest.mark.parametrize("ndim,dtype,d2h", [(3, np.uint16, "dma"), (3, np.float32, "kernel"), (2, np.uint8, "dma"),
+                                            (2, ">u2", "runtime")])
+def test_flowstream_ring_wraps(ndim, dtype, d2h):
+    """Many frames through the device ring (wraps it several times, every
+    buffer set reused) — each output equals calc_flow3D/2D of its window."""
+    from opticalflow3d_dev_amd import calc_flow2D, calc_flow3D
+    from opticalflow3d_dev_amd.stream import FlowStream
+
+    tsig = 2 if ndim == 3 else 1
+    nwin = 6 * tsig + 1
+    shape = (nwin + 9,) + ((6, 14, 22) if ndim == 3 else (40, 36))
+    stack = np.random.default_rng(5).integers(0, 250, size=shape).astype(dtype)
+    fs = FlowStream(ndim, shape[1:], np.dtype(dtype).newbyteorder("="), 1, tsig, 2, d2h=d2h)
+    try:
+        pend = []
+        for t in range(shape[0]):
+            fs.push(stack[t])
+            if fs.ready:
+                pend.append((t - nwin + 1, fs.submit()))
+                if len(pend) == fs.depth:  # keep every buffer set in flight
+                    k, p = pend.pop(0)
+                    _check_stream(p, stack[k:k + nwin], ndim, tsig, calc_flow2D, calc_flow3D)
+        for k, p in pend:
+            _check_stream(p, stack[k:k + nwin], ndim, tsig, calc_flow2D, calc_flow3D)
+    finally:
+        fs.close()
+
+
+def _check_stream(p, win, ndim, tsig, f2, f3):
+    ref = f3(win, 1, tsig, 2) if ndim == 3 else f2(win, 1, tsig, 2)
+    got = p.result()
+    for g, r in zip(got, ref):
+        assert bits_equal(g, r)
+    p.release()
+
+
+@pytest.mark.parametrize("nbytes,off", [(1, 0), (4097, 0), (1 << 20, 0), ((1 << 20) + 13, 3), (33 << 20, 0)])
+def test_copy_async_device_to_pinned(nbytes, off):
+    import torch
+    from opticalflow3d_dev_amd import _lib
+
+    src = torch.randint(0, 256, (nbytes + off,), dtype=torch.uint8, device="cuda")
+    dst = torch.zeros(nbytes + off + 7, dtype=torch.uint8).pin_memory()
+    s = torch.cuda.current_stream()
+    _lib.copy_async(dst.data_ptr() + off, src.data_ptr() + off, nbytes, 16, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(dst[off:off + nbytes], src[off:].cpu())
+    assert int(dst[:off].sum()) == 0 and int(dst[off + nbytes:].sum()) == 0
+
+
+def test_dma_copy_roundtrip():
+    import torch
+    from opticalflow3d_dev_amd import _lib
+
+    a = torch.randint(0, 256, (3 << 20,), dtype=torch.uint8, device="cuda")
+    b = torch.randint(0, 256, (4099,), dtype=torch.uint8, device="cuda")
+    ha = torch.zeros(a.numel(), dtype=torch.uint8).pin_memory()
+    hb = torch.zeros(b.numel(), dtype=torch.uint8).pin_memory()
+    torch.cuda.synchronize()
+    _lib.dma_copy([ha.data_ptr(), hb.data_ptr()], [a.data_ptr(), b.data_ptr()], [a.numel(), b.numel()])
+    assert torch.equal(ha, a.cpu()) and torch.equal(hb, b.cpu())
+    d = torch.zeros_like(a)
+    _lib.dma_copy([d.data_ptr()], [ha.data_ptr()], [a.numel()])  # host -> device too
+    assert torch.equal(d, a)
+    with pytest.raises(RuntimeError):
+        pageable = np.zeros(16, np.uint8)
+        _lib.dma_copy([pageable.ctypes.data], [a.data_ptr()], [16])
