@@ -41,7 +41,11 @@ CONFIGS = {
     # name: (Nt, Nz, Ny, Nx, xyzSig, tSig, wSig, description)
     "c2": (13, 64, 256, 256, 2, 2, 5, "configs[1]: 3D OneTif 256x256x64 x13 frames (tSig=2), xyzSig=2 wSig=5, fp64"),
     "c3": (19, 128, 512, 512, 2, 3, 7, "configs[2]: 3D 512x512x128 x19 frames (tSig=3), xyzSig=2 wSig=7, fp64"),
+    # configs[3]: one frame z-sharded over the ranks (strong scaling), halo exchange over RCCL
+    "c4": (13, 256, 1024, 1024, 2, 2, 5, "configs[3]: 3D 1024x1024x256 x13 frames, z-slabs over the GPUs with "
+                                         "RCCL halo exchange (sigmas as c2, SURVEY §8d), fp64"),
 }
+ZSLAB_CONFIGS = ("c4",)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOP/s fp64 vector counts an FMA as 2; add/mul issue at half
@@ -64,6 +68,35 @@ def synthetic_frames(nt, nz, ny, nx, seed):
                      * np.sin(k[q, 2] * (z - vel[2] * t) + ph[q, 2]))
         noise = rng.integers(-8, 9, size=(nz, ny, nx))
         out[t] = np.clip(1000 + 300 * s + noise, 0, 65535).astype(np.uint16)
+    return out
+
+
+def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device):
+    """Planes [z0, z1) of a device-generated uint16 stack of the same family as
+    synthetic_frames (for the large configs: each rank generates only its own
+    planes, and the planes do not depend on the decomposition).  Returned as
+    int16 bits (values stay below 32768)."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    k = rng.uniform(2 * np.pi / 24, 2 * np.pi / 6, size=(3, 3))
+    ph = rng.uniform(0, 2 * np.pi, size=(3, 3))
+    vel = (0.3, -0.2, -0.1)
+    f64 = dict(dtype=torch.float64, device=device)
+    z = torch.arange(z0, z1, **f64)[:, None, None]
+    y = torch.arange(ny, **f64)[None, :, None]
+    x = torch.arange(nx, **f64)[None, None, :]
+    lin = ((torch.arange(z0, z1, device=device)[:, None, None] * ny
+            + torch.arange(ny, device=device)[None, :, None]) * nx + torch.arange(nx, device=device)[None, None, :])
+    out = torch.empty((nt, z1 - z0, ny, nx), dtype=torch.int16, device=device)
+    for t in range(nt):
+        sv = torch.zeros((z1 - z0, ny, nx), **f64)
+        for q in range(3):
+            sv += (torch.sin(k[q, 0] * (x - vel[0] * t) + ph[q, 0]) * torch.sin(k[q, 1] * (y - vel[1] * t) + ph[q, 1])
+                   * torch.sin(k[q, 2] * (z - vel[2] * t) + ph[q, 2]))
+        idx = lin + t * nz * ny * nx
+        noise = ((idx ^ (idx >> 7)) * 747796405 + 2891336453) % 17 - 8
+        out[t] = torch.clamp(1000 + 300 * sv + noise, 0, 32767).to(torch.int16)
     return out
 
 
@@ -106,19 +139,22 @@ def load_pmc_traffic(stage, cfg):
         return None
 
 
-def cpu_baseline(frames, s, t, w, budget_s):
+def cpu_sample_planes(nz, ny, nx, budget_s):
+    """z-planes of the bounded CPU sample: the whole frame if it fits the budget, else a z-subvolume."""
+    est = nz * ny * nx / 0.25e6  # ~0.25 Mvox/s on one core
+    return nz if est <= budget_s else max(8, int(nz * budget_s / est))
+
+
+def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
     """Time the oracle (scipy correlate1d + LAPACK cgeev, the reference's primitives) on 1 thread."""
     from threadpoolctl import threadpool_limits
 
     from oracle import cpu_ref
 
     nt, nz, ny, nx = frames.shape
+    nz = nz_total or nz
     with threadpool_limits(limits=1):
-        # bounded sample: whole frame if it fits the budget estimate, else a z-subvolume
-        sub_nz = nz
-        est = nz * ny * nx / 0.25e6  # ~0.25 Mvox/s on one core
-        if est > budget_s:
-            sub_nz = max(8, int(nz * budget_s / est))
+        sub_nz = min(cpu_sample_planes(nz, ny, nx, budget_s), frames.shape[1])
         sample = frames[:, :sub_nz]
         t0 = time.perf_counter()
         cpu_ref.calc_flow3D(sample, s, t, w, backend="scipy")
@@ -129,6 +165,104 @@ def cpu_baseline(frames, s, t, w, budget_s):
             "sample": f"{what} ({sub_nz}x{ny}x{nx} voxels, {nt} frames): oracle/cpu_ref.py calc_flow3D with "
                       f"scipy.ndimage.correlate1d + numpy.linalg.eigvals(complex64), 1 thread, {dt:.2f} s",
             "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
+
+
+def roofline(stages, model, cfg, frame_bytes, nwin):
+    """roofline object of the bench line: the dominant stage (HIP-event average over the timed
+    region) against HBM peak, with its PMC traffic, plus the whole-frame figure."""
+    dom = max(stages, key=stages.get)
+    dom_ms = stages[dom]
+    ach = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
+    frame_ms = sum(stages.values())
+    return {
+        "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, cfg),
+        "algorithmic_bytes_per_launch": model[dom]["bytes"], "avg_launch_ms": round(dom_ms, 5),
+        "valu_fp64_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
+        "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+        "stage_ms": {k: round(v, 5) for k, v in stages.items()},
+        "frame": {"bytes_per_voxel": nwin * 2 + 3 * 8 + 4, "device_ms": round(frame_ms, 4),
+                  "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
+                  "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+    }
+
+
+def run_zslab(args, world, rank, local_rank, dev):
+    """configs[3]: ONE frame per step, z-sharded over the ranks (strong scaling).  Each rank
+    generates only its own input planes; every step fetches the rd+rw halo planes from the
+    z-neighbours (RCCL P2P over xGMI) and computes its output planes (shard.ZSlabFlow)."""
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd import _lib, radii
+    from opticalflow3d_dev_amd.shard import ZSlabFlow
+
+    nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
+    rd, rs, rt, rw = radii(s, t, w)
+    nwin = 2 * rt + 1
+    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=local_rank, timing=max(args.steps, 1))
+    own = zf.allocate(torch.int16, dev)
+    seed = 20260206 + 4
+    own.copy_(synthetic_slab(nwin, nz, ny, nx, zf.z0, zf.z1, seed, dev))
+    n_out = max(zf.z1 - zf.z0, 0) * ny * nx
+    outs = [torch.empty(max(n_out, 1), dtype=torch.float64, device=dev) for _ in range(3)]
+    rel = torch.empty(max(n_out, 1), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        zf.run(_lib.OF3D_U16, *outs, rel, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if zf.runner is not None:
+        try:
+            zf.runner.plan.stage_times()
+        except RuntimeError:
+            pass
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = zf.runner.plan.stage_times() if zf.runner is not None else {}
+    finite = bool(torch.isfinite(outs[0][:n_out]).all().item()) if n_out else True
+    if world > 1:
+        tt = torch.tensor([elapsed, 0.0 if finite else 1.0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, finite = float(tt[0].item()), tt[1].item() == 0.0
+    if rank == 0:
+        vox = nz * ny * nx
+        nb, no = zf.zi1 - zf.zi0, zf.z1 - zf.z0
+        ng = min(zf.z1 + rw, nz) - max(zf.z0 - rw, 0)
+        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx), args.config,
+                        (nwin * 2 + 3 * 8 + 4) * no * ny * nx, nwin)
+        roof["frame"]["note"] = "rank 0's slab (output planes %d..%d, input planes %d..%d)" % (
+            zf.z0, zf.z1, zf.zi0, zf.zi1)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
+            host = synthetic_slab(nwin, nz, ny, nx, 0, sub, seed, dev).cpu().numpy().view(np.uint16)
+            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz)
+        line = {
+            "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
+            "value": round(vox * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
+                       "wSig": w, "parallelism": f"z-slabs x{world}, halo {rd + rw} planes" if world > 1
+                       else "single GPU (whole frame)", "inputs": "own z-planes of 2*rt+1 uint16 frames "
+                       "resident in HBM; halo exchange inside the timed step", "outputs_finite": finite},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    zf.close()
 
 
 def main():
@@ -157,6 +291,11 @@ def main():
     else:
         torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if args.config in ZSLAB_CONFIGS:
+        run_zslab(args, world, rank, local_rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
@@ -207,25 +346,8 @@ def main():
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         value = world * vox * args.steps / elapsed / 1e6
-        plane = ny * nx
-        model = stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, plane)
-        dom = max(stages, key=stages.get)
-        dom_ms = stages[dom]
-        ach = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
-        traffic = load_pmc_traffic(dom, args.config)
-        frame_bytes = (nwin * 2 + 3 * 8 + 4) * vox  # B = nt*s_in + 3*s_v + s_rel
-        frame_ms = sum(stages.values())
-        roof = {
-            "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "algorithmic_bytes_per_launch": model[dom]["bytes"], "avg_launch_ms": round(dom_ms, 5),
-            "valu_fp64_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
-            "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
-            "stage_ms": {k: round(v, 5) for k, v in stages.items()},
-            "frame": {"bytes_per_voxel": nwin * 2 + 3 * 8 + 4, "device_ms": round(frame_ms, 4),
-                      "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
-                      "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-        }
+        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx), args.config,
+                        (nwin * 2 + 3 * 8 + 4) * vox, nwin)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(frames, s, t, w, args.cpu_budget)

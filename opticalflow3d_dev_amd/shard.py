@@ -47,6 +47,14 @@ def halo_planes(nz: int, z0: int, z1: int, rd: int, rw: int) -> tuple:
     return max(z0 - h, 0), min(z1 + h, nz)
 
 
+def _bytes(t):
+    """Byte view of a contiguous tensor: NCCL/RCCL has no 16-bit integer type, so the
+    frames (uint16 bits in int16 tensors) travel as uint8."""
+    import torch
+
+    return t.reshape(-1).view(torch.uint8)
+
+
 def exchange_halos(local, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
     """Assemble the input planes [max(z0-halo,0), min(z1+halo,nz)) of this rank.
 
@@ -70,7 +78,7 @@ def exchange_halos(local, z0: int, z1: int, nz: int, halo: int, rank: int, world
         s0, s1 = max(need0, z0), min(need1, z1)
         if s1 > s0:
             send = local[..., s0 - z0:s1 - z0, :, :].contiguous()
-            ops.append(dist.P2POp(dist.isend, send, r, group))
+            ops.append(dist.P2POp(dist.isend, _bytes(send), r, group))
         # planes I need from rank r
         g0, g1 = max(zi0, rz0), min(zi1, rz1)
         if g1 > g0:
@@ -78,7 +86,7 @@ def exchange_halos(local, z0: int, z1: int, nz: int, halo: int, rank: int, world
             shape[-3] = g1 - g0
             buf = torch.empty(shape, dtype=local.dtype, device=local.device)
             recv[r] = (g0, g1, buf)
-            ops.append(dist.P2POp(dist.irecv, buf, r, group))
+            ops.append(dist.P2POp(dist.irecv, _bytes(buf), r, group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -114,6 +122,86 @@ class SlabRunner:
 
     def close(self):
         self.plan.close()
+
+
+def fill_halos(block, zi0: int, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
+    """In-place form of exchange_halos: ``block`` (..., zi1-zi0, Ny, Nx) already
+    holds this rank's planes [z0, z1) at offset z0-zi0; the halo planes are
+    received from the neighbours into it (and this rank's boundary planes sent
+    from it).  Only halo-sized temporaries are allocated."""
+    import torch
+    import torch.distributed as dist
+
+    zi1 = zi0 + block.shape[-3]
+    # gloo moves host tensors only: stage CUDA planes through host memory there
+    stage = block.is_cuda and dist.get_backend(group) == "gloo"
+    bounds = [zslab_bounds(nz, r, world) for r in range(world)]
+    ops, recv = [], []
+    for r in range(world):
+        if r == rank:
+            continue
+        rz0, rz1 = bounds[r]
+        if rz1 <= rz0:
+            continue
+        need0, need1 = max(rz0 - halo, 0), min(rz1 + halo, nz)
+        s0, s1 = max(need0, z0), min(need1, z1)
+        if s1 > s0:
+            send = block[..., s0 - zi0:s1 - zi0, :, :].contiguous()
+            ops.append(dist.P2POp(dist.isend, _bytes(send.cpu() if stage else send), r, group))
+        g0, g1 = max(zi0, rz0), min(zi1, rz1)
+        if g1 > g0:
+            shape = list(block.shape)
+            shape[-3] = g1 - g0
+            buf = torch.empty(shape, dtype=block.dtype, device="cpu" if stage else block.device)
+            recv.append((g0, g1, buf))
+            ops.append(dist.P2POp(dist.irecv, _bytes(buf), r, group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for g0, g1, buf in recv:
+        block[..., g0 - zi0:g1 - zi0, :, :].copy_(buf)
+    return block
+
+
+class ZSlabFlow:
+    """One rank's share of a z-sharded frame (SURVEY §8e, configs[3]).
+
+    Each rank holds only its own input planes [z0, z1) of the 2*rt+1 frames
+    (as it would after reading its z-range of the TIFF), written into
+    ``own`` — a view of the rank's input block [zi0, zi1).  run() fetches the
+    H = rd + rw halo planes from the z-neighbours with torch.distributed P2P
+    (RCCL over xGMI for CUDA tensors) into the block, then computes output
+    planes [z0, z1) — bit-identical to the unsharded frame.  Outputs stay on
+    this rank (no gather)."""
+
+    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, rank, world, device=0, timing=0, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.z0, self.z1 = zslab_bounds(nz, rank, world)
+        self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
+        self.halo = self.rd + self.rw
+        self.nz, self.ny, self.nx = nz, ny, nx
+        self.runner = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, self.z0, self.z1, device=device, timing=timing) \
+            if self.z1 > self.z0 else None
+        self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw)
+        if self.runner is not None:
+            assert (self.runner.zi0, self.runner.zi1) == (self.zi0, self.zi1)
+        self.block = None
+
+    def allocate(self, dtype, device):
+        """Input block (2rt+1, zi1-zi0, ny, nx); returns the view of this rank's own planes."""
+        import torch
+
+        self.block = torch.empty((2 * self.rt + 1, self.zi1 - self.zi0, self.ny, self.nx), dtype=dtype, device=device)
+        return self.block[:, self.z0 - self.zi0:self.z1 - self.zi0]
+
+    def run(self, dtype_code, vx, vy, vz, rel, stream=0):
+        fill_halos(self.block, self.zi0, self.z0, self.z1, self.nz, self.halo, self.rank, self.world, self.group)
+        if self.runner is not None:
+            self.runner.run(self.block, dtype_code, vx, vy, vz, rel, stream)
+
+    def close(self):
+        if self.runner is not None:
+            self.runner.close()
 
 
 def flow3d_zslabs_host(images, xyzSig, tSig, wSig, world, device=0):

@@ -29,3 +29,62 @@ def test_plan_input_range_matches_python():
             z0, z1 = zslab_bounds(64, r, world)
             assert plan.input_range(z0, z1) == halo_planes(64, z0, z1, rd, rw)
     plan.close()
+
+
+def _zslab_worker(rank, world, port, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd.shard import ZSlabFlow
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        img = np.random.default_rng(7).integers(0, 4096, size=(13, 30, 20, 24)).astype(np.uint16)
+        dev = torch.device("cuda", 0)
+        zf = ZSlabFlow(30, 20, 24, 2, 2, 5, rank, world, device=0)
+        own = zf.allocate(torch.int16, dev)
+        own.copy_(torch.from_numpy(img[:, zf.z0:zf.z1].view(np.int16)))
+        n = (zf.z1 - zf.z0) * 20 * 24
+        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
+        rel = torch.empty(n, dtype=torch.float32, device=dev)
+        zf.run(_lib.OF3D_U16, *outs, rel, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        q.put((rank, zf.z0, zf.z1, [t.cpu().numpy() for t in outs + [rel]]))
+        zf.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_zslab_ranks_with_halo_exchange(world):
+    """ZSlabFlow as bench.py's c4 path runs it: each rank holds only its own
+    planes, fetches halos from its neighbours (gloo here, staged through host
+    memory; RCCL on a multi-GPU node), and its slab equals the same planes of
+    the unsharded frame bit for bit."""
+    import multiprocessing as mp
+    import socket
+
+    img = np.random.default_rng(7).integers(0, 4096, size=(13, 30, 20, 24)).astype(np.uint16)
+    full = calc_flow3D(img, 2, 2, 5)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_zslab_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    covered = 0
+    for rank, z0, z1, outs in res:
+        covered += z1 - z0
+        for a, b in zip(full, outs):
+            assert bits_equal(a[z0:z1], b.reshape(z1 - z0, 20, 24))
+    assert covered == 30

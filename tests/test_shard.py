@@ -9,7 +9,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from opticalflow3d_dev_amd.shard import exchange_halos, frame_assignment, halo_planes, zslab_bounds
+from opticalflow3d_dev_amd.shard import exchange_halos, frame_assignment, halo_planes, zslab_bounds, fill_halos
 
 
 @pytest.mark.parametrize("nz,world", [(64, 1), (64, 2), (64, 3), (7, 8), (256, 4), (5, 5), (1, 2)])
@@ -64,6 +64,38 @@ def test_exchange_halos_gloo(world, nz, halo):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, nz, halo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
+
+
+def _fill_worker(rank, world, port, nz, rd, rw, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = torch.arange(3 * nz * 4 * 5, dtype=torch.int16).reshape(3, nz, 4, 5)
+        z0, z1 = zslab_bounds(nz, rank, world)
+        zi0, zi1 = halo_planes(nz, z0, z1, rd, rw)
+        block = torch.full((3, zi1 - zi0, 4, 5), -1, dtype=torch.int16)
+        block[:, z0 - zi0:z1 - zi0] = full[:, z0:z1]
+        fill_halos(block, zi0, z0, z1, nz, rd + rw, rank, world)
+        q.put((rank, bool(torch.equal(block, full[:, zi0:zi1]))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nz,rd,rw", [(2, 16, 1, 2), (3, 20, 2, 3), (4, 9, 1, 3), (4, 3, 1, 1), (2, 64, 6, 15)])
+def test_fill_halos_gloo(world, nz, rd, rw):
+    """In-place halo fill used by ZSlabFlow (bench.py c4): every rank's block
+    equals the global stack over [zi0, zi1), including empty slabs (world > nz)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fill_worker, args=(r, world, port, nz, rd, rw, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
