@@ -462,16 +462,21 @@ constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64;
 
 // Streaming form: a block owns 64 rows of one plane and one field, and marches
 // along x K4_TX columns at a time.  The LDS window holds columns
-// x' = x0 .. x0 + K4_TX + 2rw - 1 (x' = x + rw) of every row (odd pitch so
-// lane = row reads are conflict-free); after each step the last 2rw columns
-// move to the front.  Results leave through a transposing LDS tile for
+// x' = x0 .. x0 + K4_TX + 2ha - 1 (x' = x + ha) of every row, ha = rw rounded
+// up to 16 columns, so every 32-column fetch starts on a 128-byte line (odd
+// pitch so lane = row reads are conflict-free); after each step the last 2ha
+// columns move to the front.  Results leave through a transposing LDS tile for
 // coalesced row stores; the next step's columns are fetched into registers
 // during the current pass.
-template <int NF, int TJ>  // TJ >= ceil(2rw / 32): tail column groups per loader lane
-__global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, double* __restrict__ Q, int ny, int nx,
-                                            size_t fs, const double* __restrict__ hw, int rw) {
+constexpr int k4_halo(int rw) { return (rw + 15) & ~15; }
+
+template <int NF, int TJ>  // TJ >= ceil(2ha / 32): tail column groups per loader lane
+__global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const double* __restrict__ P, double* __restrict__ Q,
+                                                             int ny, int nx, size_t fs,
+                                                             const double* __restrict__ hw, int rw) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
-    const int h2 = 2 * rw;
+    const int ha = k4_halo(rw);
+    const int h2 = 2 * ha;
     const int PP = (K4_TX + h2) | 1;
     constexpr int OP = K4_TX + 1;
     double* so = sm + K4_ROWS * PP;  // output tile [row][K4_TX]
@@ -483,10 +488,10 @@ __global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, dou
     double* dst = Q + f * fs + pl;
     // loader mapping: lanes 0..31 / 32..63 -> two rows, 32 consecutive columns
     const int lc = lane & 31, lr = (lane >> 5) + 2 * g;  // rows lr, lr + 8, ..., lr + 56
-    const double* rowp[8];
+    int roff[8];  // row offsets (ny * nx < 2^31 per plan)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rowp[j] = src + (size_t)min(y0 + lr + 8 * j, ny - 1) * nx;
-    auto colv = [&](int j, int xp) { return rowp[j][clampi(xp - rw, 0, nx - 1)]; };
+    for (int j = 0; j < 8; ++j) roff[j] = min(y0 + lr + 8 * j, ny - 1) * nx;
+    auto colv = [&](int j, int xp) { return src[roff[j] + clampi(xp - ha, 0, nx - 1)]; };
     for (int xp = lc; xp < h2; xp += 32)
 #pragma unroll
         for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + xp] = colv(j, xp);
@@ -504,7 +509,7 @@ __global__ __launch_bounds__(256, 3) void k_wx(const double* __restrict__ P, dou
         const bool more = x0 + K4_TX < nx;
         if (more) fetch(x0 + K4_TX + h2);
         double out[K4_R];
-        lds_pass<K4_R, false>(sm + lane * PP, 1, rw + g * K4_R, hw, rw, out);
+        lds_pass<K4_R, false>(sm + lane * PP, 1, ha + g * K4_R, hw, rw, out);
 #pragma unroll
         for (int i = 0; i < K4_R; ++i) so[lane * OP + g * K4_R + i] = out[i];
         if (more) {
@@ -593,7 +598,10 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
 // field's pass); each thread keeps its K5_R outputs of all 9 fields in
 // registers for the pointwise solve.
 constexpr int K5_G = 8;  // 512-thread blocks: 64 lanes x 8 z-groups x R planes (R = 8 for rw <= 16, else 4)
-constexpr int k5_r(int rw) { return rw <= 16 ? 8 : 4; }
+#ifndef OF3D_K5_R8_MAX
+#define OF3D_K5_R8_MAX 24
+#endif
+constexpr int k5_r(int rw) { return rw <= OF3D_K5_R8_MAX ? 8 : 4; }
 
 template <typename RelT, int NJ, int K5_R>
 __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
@@ -834,7 +842,10 @@ int nj_for(int h) { return h <= 64 ? 16 : (h <= 80 ? 20 : (h <= 96 ? 24 : 32)); 
 template <typename RelT>
 const void* k5_kernel(int rw) {
     // rows per thread of the staged window: ceil((K5_G * R + 2rw) / K5_G)
-    if (k5_r(rw) == 8) return (const void*)k_wz_solve<RelT, 12, 8>;  // rw <= 16: (64 + 32) / 8
+    if (k5_r(rw) == 8) {
+        if (rw <= 16) return (const void*)k_wz_solve<RelT, 12, 8>;  // (64 + 32) / 8
+        return (const void*)k_wz_solve<RelT, 14, 8>;                // rw <= 24: (64 + 48) / 8
+    }
     const int nj = (K5_G * 4 + 2 * rw + K5_G - 1) / K5_G;
     switch (nj <= 10 ? 10 : (nj <= 12 ? 12 : 16)) {
         case 10: return (const void*)k_wz_solve<RelT, 10, 4>;
@@ -856,7 +867,7 @@ const void* k3_kernel(int np, int rw) {
 }
 
 const void* k4_kernel(int nf, int rw) {
-    const int tj = (2 * rw + 31) / 32;  // <= 3 for rw <= 48
+    const int tj = (2 * k4_halo(rw) + 31) / 32;  // <= 3 for rw <= 48
     if (nf == 9) return tj <= 1 ? (const void*)k_wx<9, 1> : (tj == 2 ? (const void*)k_wx<9, 2> : (const void*)k_wx<9, 3>);
     return tj <= 1 ? (const void*)k_wx<5, 1> : (tj == 2 ? (const void*)k_wx<5, 2> : (const void*)k_wx<5, 3>);
 }
@@ -867,7 +878,7 @@ int set_attrs(of3d_plan* p) {
     p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * sizeof(double);
     p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
     p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
-    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * p->rw) | 1) + (K4_TX + 1)) * sizeof(double);
+    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * sizeof(double);
     p->k5_lds = (size_t)2 * (K5_G * k5_r(p->rw) + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
