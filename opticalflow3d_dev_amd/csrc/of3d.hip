@@ -597,13 +597,34 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
 // staged in LDS (double-buffered, next field's loads in flight during this
 // field's pass); each thread keeps its K5_R outputs of all 9 fields in
 // registers for the pointwise solve.
-constexpr int K5_G = 8;  // 512-thread blocks: 64 lanes x 8 z-groups x R planes (R = 8 for rw <= 16, else 4)
-#ifndef OF3D_K5_R8_MAX
-#define OF3D_K5_R8_MAX 24
-#endif
-constexpr int k5_r(int rw) { return rw <= OF3D_K5_R8_MAX ? 8 : 4; }
+// Geometry: 64 lanes x G z-groups x R planes per thread (z-block of G*R planes).
+// R = 8, G = 8 up to rw 24 (64-plane blocks), else R = 4, G = 8.
+struct K5Geom {
+    int r, g;
+};
+constexpr K5Geom k5_geom(int rw) { return {rw <= 24 ? 8 : 4, 8}; }
 
-template <typename RelT, int NJ, int K5_R>
+// Pointwise tail of K5: solve + reliability for the thread's R planes.
+template <typename RelT, int K5_R>
+__device__ __forceinline__ void k5_solve_store(const double (&acc)[9][K5_R], int z0l, int nzo, size_t o0, size_t ps,
+                                               double* __restrict__ vx, double* __restrict__ vy,
+                                               double* __restrict__ vz, RelT* __restrict__ rel) {
+#pragma unroll
+    for (int i = 0; i < K5_R; ++i) {
+        if (z0l + i >= nzo) break;
+        // field order: tx ty tz xy xz x2 yz y2 z2
+        double ox, oy, oz;
+        solve3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i], acc[0][i], acc[1][i], acc[2][i], ox,
+               oy, oz);
+        const size_t o = (size_t)(z0l + i) * ps + o0;
+        vx[o] = ox;
+        vy[o] = oy;
+        vz[o] = oz;
+        rel[o] = (RelT)eigmin3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i]);
+    }
+}
+
+template <typename RelT, int NJ, int K5_R, int K5_G>
 __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
                                                   size_t fs, const double* __restrict__ hw, int rw, int zo0, int nzo,
                                                   double* __restrict__ vx, double* __restrict__ vy,
@@ -641,24 +662,76 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict
         lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
     }
     if (x >= nx) return;
+    k5_solve_store<RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
+}
+
+// 16-byte global -> LDS copy (LDS-DMA): lane i's 16 bytes land at lds_byte + 16 i.
+// Inline asm keeps it out of the compiler's wait bookkeeping (the compiler
+// would drain it with vmcnt(0) before every LDS read); waits are explicit.
+__device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_byte)
+                 : "memory");
+}
+
+// K5 with LDS-DMA staging: the field windows are loaded straight into NB LDS
+// buffers, NB - 1 fields ahead of the pass (no staging registers, no VGPR cost
+// for the prefetch), so a CU keeps up to (NB - 1) x 48 KB of loads in flight
+// instead of one field.  Lanes 0-31 / 32-63 of a wave load rows 2p / 2p+1 of
+// the window as 16-byte column pairs.  Needs nx even (16-byte aligned rows).
+// (A persistent form that also prefetches the next tile during the epilogue
+// spilled registers and measured slower.)
+template <typename RelT, int NJ2, int K5_R, int K5_G, int NB>
+__global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const double* __restrict__ Q, int zq0, int nz, int ny,
+                                                      int nx, size_t fs, const double* __restrict__ hw, int rw,
+                                                      int zo0, int nzo, double* __restrict__ vx,
+                                                      double* __restrict__ vy, double* __restrict__ vz,
+                                                      RelT* __restrict__ rel) {
+    constexpr int K5_ZC = K5_G * K5_R;
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    const int H = K5_ZC + 2 * rw;
+    const int H2 = (H + 1) >> 1;  // row pairs per window
+    const int lane = threadIdx.x, g = threadIdx.y;
+    const int x = blockIdx.x * 64 + lane;
+    const int y = blockIdx.y;
+    const int zc0 = zo0 + blockIdx.z * K5_ZC;
+    const size_t ps = (size_t)ny * nx;
+    const int xc = min((int)blockIdx.x * 64 + 2 * (lane & 31), nx - 2);  // this lane's column pair
+    const double* qrow = Q + (size_t)y * nx + xc;
+    const unsigned lds0 = (unsigned)(uintptr_t)sm;
+    auto issue = [&](int f, int b) {
+        const double* q = qrow + f * fs;
+        const unsigned lb = lds0 + (unsigned)(b * H2 * 128 * sizeof(double));
 #pragma unroll
-    for (int i = 0; i < K5_R; ++i) {
-        const int zl = zc0 + g * K5_R + i - zo0;
-        if (zl >= nzo) break;
-        // field order: tx ty tz xy xz x2 yz y2 z2
-        double ox, oy, oz;
-        solve3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i], acc[0][i], acc[1][i], acc[2][i], ox,
-               oy, oz);
-        const size_t o = (size_t)zl * ps + (size_t)y * nx + x;
-        vx[o] = ox;
-        vy[o] = oy;
-        vz[o] = oz;
-#if defined(OF3D_ABLATE_K5) && OF3D_ABLATE_K5 == 1
-        rel[o] = (RelT)(acc[5][i] + acc[7][i] + acc[8][i] + acc[3][i] + acc[4][i] + acc[6][i]);
-#else
-        rel[o] = (RelT)eigmin3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i]);
-#endif
+        for (int j = 0; j < NJ2; ++j) {
+            const int p = min(g + K5_G * j, H2 - 1);  // surplus slots repeat the last pair: equal counts per wave
+            const int row = min(2 * p + (lane >> 5), H - 1);
+            const double* src = q + (size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps;
+            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(p * 128 * sizeof(double))));
+        }
+    };
+    double acc[9][K5_R];
+#pragma unroll
+    for (int f = 0; f < NB - 1; ++f) issue(f, f);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+        // field f landed (loads of the fields issued after it may stay in flight: loads
+        // retire in issue order), and every wave is done reading the buffer the next
+        // issue overwrites
+        const int ahead = min(NB - 2, 8 - f);
+        if (ahead >= 2)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * NJ2) : "memory");
+        else if (ahead == 1)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NJ2) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
+        lds_pass<K5_R, false>(sm + (f % NB) * H2 * 128 + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
     }
+    if (x >= nx) return;
+    k5_solve_store<RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
@@ -725,6 +798,8 @@ struct of3d_plan {
     size_t fs = 0;        // field stride (elements)
     hipStream_t stream = nullptr;
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
+    int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
+    size_t k5d_lds = 0;
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
@@ -835,23 +910,39 @@ const void* k0_kernel_dt(int dtype) {
     }
 }
 
-// K5 variants: rows of the staged window each thread prefetches into
-// registers (4 row-groups): NJ >= ceil(H/4).
-int nj_for(int h) { return h <= 64 ? 16 : (h <= 80 ? 20 : (h <= 96 ? 24 : 32)); }
-
 template <typename RelT>
 const void* k5_kernel(int rw) {
-    // rows per thread of the staged window: ceil((K5_G * R + 2rw) / K5_G)
-    if (k5_r(rw) == 8) {
-        if (rw <= 16) return (const void*)k_wz_solve<RelT, 12, 8>;  // (64 + 32) / 8
-        return (const void*)k_wz_solve<RelT, 14, 8>;                // rw <= 24: (64 + 48) / 8
-    }
-    const int nj = (K5_G * 4 + 2 * rw + K5_G - 1) / K5_G;
+    // NJ = rows per thread of the staged window: ceil((G * R + 2rw) / G)
+    const K5Geom k = k5_geom(rw);
+    if (k.r == 8) return rw <= 16 ? (const void*)k_wz_solve<RelT, 12, 8, 8> : (const void*)k_wz_solve<RelT, 14, 8, 8>;
+    const int nj = (8 * 4 + 2 * rw + 7) / 8;
     switch (nj <= 10 ? 10 : (nj <= 12 ? 12 : 16)) {
-        case 10: return (const void*)k_wz_solve<RelT, 10, 4>;
-        case 12: return (const void*)k_wz_solve<RelT, 12, 4>;
-        default: return (const void*)k_wz_solve<RelT, 16, 4>;
+        case 10: return (const void*)k_wz_solve<RelT, 10, 4, 8>;
+        case 12: return (const void*)k_wz_solve<RelT, 12, 4, 8>;
+        default: return (const void*)k_wz_solve<RelT, 16, 4, 8>;
     }
+}
+
+// LDS-DMA K5: NB window buffers of ceil(H / 2) row pairs; NJ2 = pairs per wave.
+#ifndef OF3D_K5_DMA
+#define OF3D_K5_DMA 1
+#endif
+constexpr int k5_pairs(int rw) { return (k5_geom(rw).g * k5_geom(rw).r + 2 * rw + 1) / 2; }
+int k5_dma_nb(int rw) {
+    if (!OF3D_K5_DMA) return 0;
+    const size_t buf = (size_t)k5_pairs(rw) * 128 * sizeof(double), lim = 160 * 1024;
+    return 3 * buf <= lim ? 3 : (2 * buf <= lim ? 2 : 0);
+}
+
+template <typename RelT>
+const void* k5_dma_kernel(int rw, int nb) {
+    const K5Geom k = k5_geom(rw);
+    const int nj2 = (k5_pairs(rw) + k.g - 1) / k.g;
+#define OF3D_K5D(NJ2, R) \
+    (nb == 3 ? (const void*)k_wz_solve_dma<RelT, NJ2, R, 8, 3> : (const void*)k_wz_solve_dma<RelT, NJ2, R, 8, 2>)
+    if (k.r == 8) return nj2 <= 6 ? OF3D_K5D(6, 8) : OF3D_K5D(7, 8);  // rw <= 24: nj2 <= 7
+    return nj2 <= 6 ? OF3D_K5D(6, 4) : (nj2 <= 7 ? OF3D_K5D(7, 4) : OF3D_K5D(8, 4));  // rw <= 48: nj2 <= 8
+#undef OF3D_K5D
 }
 
 const void* k3_kernel(int np, int rw) {
@@ -879,7 +970,7 @@ int set_attrs(of3d_plan* p) {
     p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
     p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
     p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * sizeof(double);
-    p->k5_lds = (size_t)2 * (K5_G * k5_r(p->rw) + 2 * p->rw) * 64 * sizeof(double);
+    p->k5_lds = (size_t)2 * (k5_geom(p->rw).g * k5_geom(p->rw).r + 2 * p->rw) * 64 * sizeof(double);
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
     auto attr = [&](const void* k, size_t b) -> int {
@@ -892,6 +983,12 @@ int set_attrs(of3d_plan* p) {
     rc |= attr(k3_kernel(9, p->rw), p->k3_lds) | attr(k3_kernel(5, p->rw), p->k3_lds);
     rc |= attr(k4_kernel(9, p->rw), p->k4_lds) | attr(k4_kernel(5, p->rw), p->k4_lds);
     rc |= attr(k5_kernel<float>(p->rw), p->k5_lds) | attr(k5_kernel<double>(p->rw), p->k5_lds);
+    p->k5_nb = (p->nx % 2 == 0 && p->nx >= 2) ? k5_dma_nb(p->rw) : 0;
+    if (p->k5_nb) {
+        p->k5d_lds = (size_t)p->k5_nb * k5_pairs(p->rw) * 128 * sizeof(double);
+        rc |= attr(k5_dma_kernel<float>(p->rw, p->k5_nb), p->k5d_lds) |
+              attr(k5_dma_kernel<double>(p->rw, p->k5_nb), p->k5d_lds);
+    }
     return rc ? -1 : 0;
 }
 
@@ -1010,13 +1107,19 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {
-        dim3 g(cdiv(nx, 64), ny, cdiv(no, K5_G * k5_r(p->rw)));
+        const K5Geom kg = k5_geom(p->rw);
+        dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
         int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
         const double* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-        const void* k5 = p->rel64 ? k5_kernel<double>(p->rw) : k5_kernel<float>(p->rw);
-        OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, K5_G), args, p->k5_lds, s));
+        if (p->k5_nb) {
+            const void* k5 = p->rel64 ? k5_dma_kernel<double>(p->rw, p->k5_nb) : k5_dma_kernel<float>(p->rw, p->k5_nb);
+            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
+        } else {
+            const void* k5 = p->rel64 ? k5_kernel<double>(p->rw) : k5_kernel<float>(p->rw);
+            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5_lds, s));
+        }
     } else {
         const int n = ny * nx;
         hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);
