@@ -44,11 +44,15 @@ CONFIGS = {
     # configs[3]: one frame z-sharded over the ranks (strong scaling), halo exchange over RCCL
     "c4": (13, 256, 1024, 1024, 2, 2, 5, "configs[3]: 3D 1024x1024x256 x13 frames, z-slabs over the GPUs with "
                                          "RCCL halo exchange (sigmas as c2, SURVEY §8d), fp64"),
+    "c5": (13, 512, 2048, 2048, 2, 2, 5, "configs[4]: 3D 2048x2048x512 x13 frames, fp32 path (OF3D_FP32), z-slabs "
+                                         "over the GPUs with RCCL halo exchange (sigmas as c2, SURVEY §8d)"),
 }
-ZSLAB_CONFIGS = ("c4",)
+ZSLAB_CONFIGS = ("c4", "c5")
+FP32_CONFIGS = ("c5",)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TOPS = 39.3     # 78.6 TFLOP/s fp64 vector counts an FMA as 2; add/mul issue at half
+FP32_VALU_PEAK_TOPS = 78.6     # 157.3 TFLOP/s fp32 vector, same convention
 
 
 def synthetic_frames(nt, nz, ny, nx, seed):
@@ -71,11 +75,12 @@ def synthetic_frames(nt, nz, ny, nx, seed):
     return out
 
 
-def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device):
+def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device, out=None, zchunk=32):
     """Planes [z0, z1) of a device-generated uint16 stack of the same family as
     synthetic_frames (for the large configs: each rank generates only its own
     planes, and the planes do not depend on the decomposition).  Returned as
-    int16 bits (values stay below 32768)."""
+    int16 bits (values stay below 32768); generated zchunk planes at a time so
+    the fp64 temporaries stay small next to a c5 workspace."""
     import torch
 
     rng = np.random.default_rng(seed)
@@ -83,37 +88,42 @@ def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device):
     ph = rng.uniform(0, 2 * np.pi, size=(3, 3))
     vel = (0.3, -0.2, -0.1)
     f64 = dict(dtype=torch.float64, device=device)
-    z = torch.arange(z0, z1, **f64)[:, None, None]
+    if out is None:
+        out = torch.empty((nt, z1 - z0, ny, nx), dtype=torch.int16, device=device)
     y = torch.arange(ny, **f64)[None, :, None]
     x = torch.arange(nx, **f64)[None, None, :]
-    lin = ((torch.arange(z0, z1, device=device)[:, None, None] * ny
-            + torch.arange(ny, device=device)[None, :, None]) * nx + torch.arange(nx, device=device)[None, None, :])
-    out = torch.empty((nt, z1 - z0, ny, nx), dtype=torch.int16, device=device)
-    for t in range(nt):
-        sv = torch.zeros((z1 - z0, ny, nx), **f64)
-        for q in range(3):
-            sv += (torch.sin(k[q, 0] * (x - vel[0] * t) + ph[q, 0]) * torch.sin(k[q, 1] * (y - vel[1] * t) + ph[q, 1])
-                   * torch.sin(k[q, 2] * (z - vel[2] * t) + ph[q, 2]))
-        idx = lin + t * nz * ny * nx
-        noise = ((idx ^ (idx >> 7)) * 747796405 + 2891336453) % 17 - 8
-        out[t] = torch.clamp(1000 + 300 * sv + noise, 0, 32767).to(torch.int16)
+    for c0 in range(z0, z1, zchunk):
+        c1 = min(c0 + zchunk, z1)
+        z = torch.arange(c0, c1, **f64)[:, None, None]
+        lin = ((torch.arange(c0, c1, device=device)[:, None, None] * ny
+                + torch.arange(ny, device=device)[None, :, None]) * nx + torch.arange(nx, device=device)[None, None, :])
+        for t in range(nt):
+            sv = torch.zeros((c1 - c0, ny, nx), **f64)
+            for q in range(3):
+                sv += (torch.sin(k[q, 0] * (x - vel[0] * t) + ph[q, 0])
+                       * torch.sin(k[q, 1] * (y - vel[1] * t) + ph[q, 1])
+                       * torch.sin(k[q, 2] * (z - vel[2] * t) + ph[q, 2]))
+            idx = lin + t * nz * ny * nx
+            noise = ((idx ^ (idx >> 7)) * 747796405 + 2891336453) % 17 - 8
+            out[t, c0 - z0:c1 - z0] = torch.clamp(1000 + 300 * sv + noise, 0, 32767).to(torch.int16)
     return out
 
 
-def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane):
-    """Algorithmic HBM bytes and fp64 VALU ops per launch of each stage.
+def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane, sv=8):
+    """Algorithmic HBM bytes and VALU ops per launch of each stage.
 
     Bytes are the compulsory reads + writes of the stage's own inputs/outputs
-    (each element once); ops count every add and multiply of the scipy-order
-    passes (C(r) = 1 + 3r per symmetric/antisymmetric output)."""
+    (each element once; sv = bytes per workspace/output value: 8 fp64, 4 fp32);
+    ops count every add and multiply of the scipy-order passes (C(r) = 1 + 3r
+    per symmetric/antisymmetric output)."""
     C = lambda r: 1 + 3 * r
     return {
-        "grad_xy": {"bytes": (nt_win * 2 + 4 * 8) * nb * plane,
+        "grad_xy": {"bytes": (nt_win * 2 + 4 * sv) * nb * plane,
                     "ops": (C(rt) + C(rd) * 2 + C(rs) + C(rd) * 2 + C(rs) * 2) * nb * plane},
-        "grad_z": {"bytes": (4 * 8 + 4 * 8) * ng * plane, "ops": (C(rd) * 2 + C(rs) * 2) * ng * plane},
-        "prod_wy": {"bytes": (4 * 8 + 9 * 8) * ng * plane, "ops": (9 + 9 * C(rw)) * ng * plane},
-        "wx": {"bytes": (9 * 8 + 9 * 8) * ng * plane, "ops": 9 * C(rw) * ng * plane},
-        "wz_solve": {"bytes": (9 * 8 + 3 * 8 + 4) * no * plane, "ops": (9 * C(rw) + 65 + 50) * no * plane},
+        "grad_z": {"bytes": (4 * sv + 4 * sv) * ng * plane, "ops": (C(rd) * 2 + C(rs) * 2) * ng * plane},
+        "prod_wy": {"bytes": (4 * sv + 9 * sv) * ng * plane, "ops": (9 + 9 * C(rw)) * ng * plane},
+        "wx": {"bytes": (9 * sv + 9 * sv) * ng * plane, "ops": 9 * C(rw) * ng * plane},
+        "wz_solve": {"bytes": (9 * sv + 3 * sv + 4) * no * plane, "ops": (9 * C(rw) + 65 + 50) * no * plane},
     }
 
 
@@ -141,8 +151,8 @@ def load_pmc_traffic(stage, cfg):
 
 def cpu_sample_planes(nz, ny, nx, budget_s):
     """z-planes of the bounded CPU sample: the whole frame if it fits the budget, else a z-subvolume."""
-    est = nz * ny * nx / 0.25e6  # ~0.25 Mvox/s on one core
-    return nz if est <= budget_s else max(8, int(nz * budget_s / est))
+    est = nz * ny * nx / 0.5e6  # ~0.5 Mvox/s on one core (measured 0.54 at c2)
+    return nz if est <= budget_s else max(1, int(nz * budget_s / est))
 
 
 def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
@@ -167,7 +177,7 @@ def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
             "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
 
 
-def roofline(stages, model, cfg, frame_bytes, nwin):
+def roofline(stages, model, cfg, frame_bytes, nwin, sv=8):
     """roofline object of the bench line: the dominant stage (HIP-event average over the timed
     region) against HBM peak, with its PMC traffic, plus the whole-frame figure."""
     dom = max(stages, key=stages.get)
@@ -178,10 +188,11 @@ def roofline(stages, model, cfg, frame_bytes, nwin):
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, cfg),
         "algorithmic_bytes_per_launch": model[dom]["bytes"], "avg_launch_ms": round(dom_ms, 5),
-        "valu_fp64_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
-        "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TOPS, 4),
+        "valu_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
+        "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 /
+                           (FP64_VALU_PEAK_TOPS if sv == 8 else FP32_VALU_PEAK_TOPS), 4),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
-        "frame": {"bytes_per_voxel": nwin * 2 + 3 * 8 + 4, "device_ms": round(frame_ms, 4),
+        "frame": {"bytes_per_voxel": nwin * 2 + 3 * sv + 4, "device_ms": round(frame_ms, 4),
                   "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
                   "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
     }
@@ -200,12 +211,14 @@ def run_zslab(args, world, rank, local_rank, dev):
     nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
-    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=local_rank, timing=max(args.steps, 1))
+    fp32 = args.config in FP32_CONFIGS or args.precision == "fp32"
+    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=local_rank, timing=max(args.steps, 1),
+                   mode=_lib.OF3D_FP32 if fp32 else 0)
     own = zf.allocate(torch.int16, dev)
-    seed = 20260206 + 4
-    own.copy_(synthetic_slab(nwin, nz, ny, nx, zf.z0, zf.z1, seed, dev))
+    seed = 20260206 + (5 if fp32 else 4)
+    synthetic_slab(nwin, nz, ny, nx, zf.z0, zf.z1, seed, dev, out=own)
     n_out = max(zf.z1 - zf.z0, 0) * ny * nx
-    outs = [torch.empty(max(n_out, 1), dtype=torch.float64, device=dev) for _ in range(3)]
+    outs = [torch.empty(max(n_out, 1), dtype=torch.float32 if fp32 else torch.float64, device=dev) for _ in range(3)]
     rel = torch.empty(max(n_out, 1), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -240,8 +253,9 @@ def run_zslab(args, world, rank, local_rank, dev):
         vox = nz * ny * nx
         nb, no = zf.zi1 - zf.zi0, zf.z1 - zf.z0
         ng = min(zf.z1 + rw, nz) - max(zf.z0 - rw, 0)
-        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx), args.config,
-                        (nwin * 2 + 3 * 8 + 4) * no * ny * nx, nwin)
+        sv = 4 if fp32 else 8
+        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx, sv), args.config,
+                        (nwin * 2 + 3 * sv + 4) * no * ny * nx, nwin, sv)
         roof["frame"]["note"] = "rank 0's slab (output planes %d..%d, input planes %d..%d)" % (
             zf.z0, zf.z1, zf.zi0, zf.zi1)
         cpu = None
@@ -253,7 +267,7 @@ def run_zslab(args, world, rank, local_rank, dev):
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(vox * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32" if fp32 else "f64",
             "data": "synthetic",
             "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
                        "wSig": w, "parallelism": f"z-slabs x{world}, halo {rd + rw} planes" if world > 1
@@ -273,6 +287,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
+    ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
+                    help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -304,12 +320,15 @@ def main():
     win = np.ascontiguousarray(frames[c - rt:c + rt + 1])
     d_in = torch.from_numpy(win.view(np.int16)).to(dev)
     vox = nz * ny * nx
-    d_vx = torch.empty(vox, dtype=torch.float64, device=dev)
+    fp32 = args.precision == "fp32"
+    sv = 4 if fp32 else 8
+    d_vx = torch.empty(vox, dtype=torch.float32 if fp32 else torch.float64, device=dev)
     d_vy = torch.empty_like(d_vx)
     d_vz = torch.empty_like(d_vx)
     d_rel = torch.empty(vox, dtype=torch.float32, device=dev)
 
-    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=local_rank, timing=max(args.steps, 1))
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=local_rank, timing=max(args.steps, 1),
+                     mode=_lib.OF3D_FP32 if fp32 else 0)
     fptrs = [d_in[i].data_ptr() for i in range(nwin)]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -346,8 +365,8 @@ def main():
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         value = world * vox * args.steps / elapsed / 1e6
-        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx), args.config,
-                        (nwin * 2 + 3 * 8 + 4) * vox, nwin)
+        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
+                        args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox, nwin, sv)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(frames, s, t, w, args.cpu_budget)
@@ -355,7 +374,7 @@ def main():
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32" if fp32 else "f64", "data": "synthetic",
             "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
                        "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
                        "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite},

@@ -51,8 +51,12 @@ enum of3d_dtype {
 /* arithmetic mode.  FP64_EXACT: fp64, no FMA contraction, scipy summation
  * order — vx/vy/vz bit-identical to the reference.  OR in OF3D_REL_F64 to get
  * the 3D reliability as float64 (the fp64 eigen-solve before the float32
- * cast; MATLAB's calc_flow3D.m:235-236 keeps rel in double). */
-enum of3d_mode { OF3D_FP64_EXACT = 0, OF3D_REL_F64 = 0x100 };
+ * cast; MATLAB's calc_flow3D.m:235-236 keeps rel in double).
+ * OF3D_FP32 (plans only; configs[4]'s "fp32 path"): the filter passes and the
+ * structure tensor in float32 (same scipy order), the 3x3 solve and the
+ * eigenvalue in fp64, every output float32: half the workspace and HBM
+ * traffic; accuracy max|dv| <= 1e-4 max|v| against the fp64 result. */
+enum of3d_mode { OF3D_FP64_EXACT = 0, OF3D_REL_F64 = 0x100, OF3D_FP32 = 0x200 };
 
 /* Filter taps (calc_flow.py:230-267).  Each vector has 2r+1 entries. */
 typedef struct of3d_taps {
@@ -128,9 +132,10 @@ int of3d_plan_input_range(const of3d_plan* plan, int64_t z_out0, int64_t z_out1,
  *   The frames must hold the planes of of3d_plan_input_range().
  * d_vx/d_vy/d_vz: float64 (z_out1-z_out0, ny, nx) (d_vz ignored for 2D);
  * d_rel: float32 for 3D (float64 if the plan's mode has OF3D_REL_F64),
- * float64 for 2D.  stream: hipStream_t or NULL. */
+ * float64 for 2D.  OF3D_FP32 plans: every output float32.
+ * stream: hipStream_t or NULL. */
 int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, int64_t frame_z0,
-                      int64_t z_out0, int64_t z_out1, double* d_vx, double* d_vy, double* d_vz,
+                      int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz,
                       void* d_rel, void* stream);
 
 /* Per-stage timing with HIP events recorded on the launch stream.

@@ -6,7 +6,8 @@ Drop-in for the hot path of ScientistRachel/OpticalFlow3D_dev
 ``libof3d.so`` (C-ABI: include/of3d.h).
 """
 
-from .calc_flow import calc_flow, calc_flow2D, calc_flow3D, process_flow  # noqa: F401
+from .calc_flow import calc_flow, calc_flow2D, calc_flow2D_fp32, calc_flow3D, calc_flow3D_fp32, process_flow  # noqa: F401
 from .taps import make_taps, radii  # noqa: F401
 
-__all__ = ["calc_flow", "calc_flow2D", "calc_flow3D", "process_flow", "make_taps", "radii"]
+__all__ = ["calc_flow", "calc_flow2D", "calc_flow3D", "process_flow", "calc_flow2D_fp32", "calc_flow3D_fp32",
+           "make_taps", "radii"]

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("OF3D_LIB", os.path.join(_HERE, "libof3d.so"))
 OF3D_U8, OF3D_U16, OF3D_I16, OF3D_U32, OF3D_I32, OF3D_F32, OF3D_F64 = 1, 2, 3, 4, 5, 6, 7
 OF3D_FP64_EXACT = 0
 OF3D_REL_F64 = 0x100
+OF3D_FP32 = 0x200
 
 DTYPE_CODES = {
     np.dtype(np.uint8): OF3D_U8,

@@ -129,17 +129,56 @@ def calc_flow2D(images, xySig=3, tSig=1, wSig=4):
     return vx, vy, rel
 
 
+def _flow_fp32(images, ndim, xyzSig, tSig, wSig):
+    from .stream import FlowStream
+
+    _check_args(images, ndim + 1, tSig, MSG_NDIM_3D if ndim == 3 else MSG_NDIM_2D)
+    a = np.asarray(images)
+    rt = math.ceil(3 * tSig)
+    c = a.shape[0] // 2
+    dt = a.dtype.newbyteorder("=") if a.dtype.byteorder not in ("=", "|") else a.dtype
+    shape = a.shape[1:]
+    if int(np.prod(shape)) == 0:
+        out = np.empty(shape, np.float32)
+        return tuple(out.copy() for _ in range(ndim + 1))
+    fs = FlowStream(ndim, shape, dt, xyzSig, tSig, wSig, depth=1, precision="fp32")
+    try:
+        for k in range(c - rt, c + rt + 1):
+            fs.push(a[k])
+        pend = fs.submit()
+        out = tuple(o.copy() for o in pend.result())
+        pend.release()
+    finally:
+        fs.close()
+    return out
+
+
+def calc_flow3D_fp32(images, xyzSig=3, tSig=1, wSig=4):
+    """calc_flow3D on the fp32 path (OF3D_FP32, configs[4]): filter passes and
+    the structure tensor in float32 (scipy order), solve and eigenvalue in
+    fp64 on that tensor; returns float32 vx, vy, vz, rel.  Not bit-exact:
+    max|dv| <= 1e-4 max|v| against calc_flow3D on smooth data."""
+    return _flow_fp32(images, 3, xyzSig, tSig, wSig)
+
+
+def calc_flow2D_fp32(images, xySig=3, tSig=1, wSig=4):
+    """calc_flow2D on the fp32 path; float32 vx, vy, rel."""
+    return _flow_fp32(images, 2, xySig, tSig, wSig)
+
+
 def _now():
     return str(datetime.now())
 
 
-def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSig=3, tSig=1, wSig=4):
+def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSig=3, tSig=1, wSig=4,
+                 precision="fp64"):
     """Parse a TIFF time lapse, run the flow per output frame, write TIFFs.
 
     Mirrors calc_flow.py:362-625: same checks and messages, the same
     ``OpticalFlow3D/<imNameSave>/`` (or ``OpticalFlow2D``) output folder,
     ``<imNameSave>_parameters.csv`` and ``<imNameSave>_{vx,vy,[vz,]rel}_t%04d.tiff``
-    files, the same stdout lines.  Returns None."""
+    files, the same stdout lines.  Returns None.  precision="fp32" (an
+    extension; configs[4]) runs the float32 path and writes float32 TIFFs."""
     ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
     imDir = Path(imDir)
     if not imDir.is_dir():
@@ -214,14 +253,18 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
         load_frame = lambda i: tf.imread(imDir / fileList[i])
     nOut = int(Nt) - NtChunk + 1
     rt = math.ceil(3 * tSig)
+    if precision not in ("fp64", "fp32"):
+        raise ValueError("precision must be 'fp64' or 'fp32'")
     if nOut > 0 and NtChunk == 2 * rt + 1:
-        _process_stream(load_frame, nOut, NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix, names)
+        _process_stream(load_frame, nOut, NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix, names,
+                        precision)
     else:  # window and temporal taps disagree (non-integer 6*tSig+1): one upload per window
         for hh in range(0, nOut):
             loopStart = datetime.now()
             print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
             images = np.stack([load_frame(hh + jj) for jj in range(NtChunk)])
-            out = flow(images, xyzSig, tSig, wSig)
+            out = flow(images, xyzSig, tSig, wSig) if precision == "fp64" else \
+                _flow_fp32(images, spatialDimensions, xyzSig, tSig, wSig)
             _write_frame(prefix, names, hh + NtSlice, out)
             del out, images
             print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(datetime.now() - loopStart))
@@ -251,7 +294,7 @@ class _Shape:
         self.shape = shape
 
 
-def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names):
+def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names, precision="fp64"):
     """process_flow's loop on a device-resident frame ring (stream.py): one
     frame read + upload per output frame; compute, download and TIFF writing
     of consecutive frames overlap.  Files and stdout lines are the reference's
@@ -265,7 +308,7 @@ def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig
         print(_now() + ' - Processing frame ' + str(NtSlice) + '...')
         _check_args(_Shape((NtChunk,) + first.shape), ndim + 1, tSig, MSG_NDIM_3D if ndim == 3 else MSG_NDIM_2D)
     dt = first.dtype.newbyteorder('=') if first.dtype.byteorder not in ('=', '|') else first.dtype
-    fs = FlowStream(ndim, first.shape, dt, xyzSig, tSig, wSig)
+    fs = FlowStream(ndim, first.shape, dt, xyzSig, tSig, wSig, precision=precision)
 
     def finish(frame, start, start_str, pending):
         print(start_str + ' - Processing frame ' + str(frame) + '...')

@@ -57,12 +57,15 @@ constexpr double kEps = 2.220446049250313e-16;  // np.finfo(float).eps, calc_flo
 
 // Half taps on the device: h[0] = centre tap w[r], h[k] = w[r-k] (left side),
 // exactly the coefficients scipy multiplies by in the symmetric branch.
+// F = the arithmetic type of the filter passes: double (exact mode) or float
+// (OF3D_FP32 plans); taps are stored in F.
+template <typename F>
 struct DevTaps {
-    const double* g;  // gauss   (rd)
-    const double* d;  // deriv   (rd, antisymmetric)
-    const double* s;  // smooth  (rs)
-    const double* t;  // tderiv  (rt, antisymmetric)
-    const double* w;  // window  (rw)
+    const F* g;  // gauss   (rd)
+    const F* d;  // deriv   (rd, antisymmetric)
+    const F* s;  // smooth  (rs)
+    const F* t;  // tderiv  (rt, antisymmetric)
+    const F* w;  // window  (rw)
     int rd, rs, rt, rw;
 };
 
@@ -72,39 +75,9 @@ struct Frames {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-template <typename T>
-__device__ __forceinline__ double ldf(const void* p, size_t i) {
-    return (double)(reinterpret_cast<const T*>(p)[i]);
-}
-
-// One 1-D correlation along a strided axis, R consecutive outputs per thread
-// (register blocking: 2 loads per tap pair for all R outputs).  ld(i) returns
-// the value at (already clamped) axis index i.
-template <int R, bool ANTI, typename Load>
-__device__ __forceinline__ void pass_line(Load ld, int p0, int L, const double* __restrict__ h, int r,
-                                          double (&out)[R]) {
-    const int last = L - 1;
-#pragma unroll
-    for (int i = 0; i < R; ++i) out[i] = ld(clampi(p0 + i, 0, last)) * h[0];
-    double lo[R], hi[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        lo[i] = ld(clampi(p0 + i - r, 0, last));
-        hi[i] = ld(clampi(p0 + i + r, 0, last));
-    }
-    for (int k = r; k >= 1; --k) {
-        const double wk = h[k];
-#pragma unroll
-        for (int i = 0; i < R; ++i) out[i] = out[i] + (ANTI ? (lo[i] - hi[i]) : (lo[i] + hi[i])) * wk;
-        if (k > 1) {
-#pragma unroll
-            for (int i = 0; i < R - 1; ++i) lo[i] = lo[i + 1];
-            lo[R - 1] = ld(clampi(p0 + R - k, 0, last));
-#pragma unroll
-            for (int i = R - 1; i > 0; --i) hi[i] = hi[i - 1];
-            hi[0] = ld(clampi(p0 + k - 1, 0, last));
-        }
-    }
+template <typename T, typename F>
+__device__ __forceinline__ F ldf(const void* p, size_t i) {
+    return (F)(reinterpret_cast<const T*>(p)[i]);
 }
 
 // 1-D pass over a staged LDS line, R consecutive outputs per thread at line
@@ -117,15 +90,15 @@ __device__ __forceinline__ void pass_line(Load ld, int p0, int L, const double* 
 // (q+i) and (q-i); each lives in a ring of M slots (L[m % M], U[m % M]), and
 // the q loop is unrolled by M so every slot index is a compile-time constant.
 // Per step: 2 LDS reads, 3R fp64 ops, ~3R live doubles, any radius.
-template <int R, bool ANTI, int D = 1, bool WRAP = false>
-__device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, int base,
-                                         const double* __restrict__ h, int r, double (&out)[R], int wmask = 0) {
+template <int R, bool ANTI, int D = 1, bool WRAP = false, typename F>
+__device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int base, const F* __restrict__ h, int r,
+                                         F (&out)[R], int wmask = 0) {
     // WRAP: the staged line is a ring of (wmask + 1) positions (power of two)
     auto at = [&](int i) { return WRAP ? s[(i & wmask) * st] : s[i * st]; };
     // Ring of M = R + D - 1 slots per stream: the two reads issued after step q
     // are first consumed at step q + D (prefetch distance D hides LDS latency).
     constexpr int M = R + D - 1;
-    double L[M], U[M];
+    F L[M], U[M];
 #pragma unroll
     for (int i = 0; i < R; ++i) out[i] = at(base + i) * h[0];
 #pragma unroll
@@ -134,11 +107,11 @@ __device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, i
     for (int m = -(R - 1); m < D; ++m) U[((m % M) + M) % M] = at(base + r - m);  // S_hi[-(R-1) .. D-1]
     auto step = [&](int q, auto jc) {  // phase j = q mod M (compile-time)
         constexpr int j = decltype(jc)::value;
-        const double wk = h[r - q];
+        const F wk = h[r - q];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            const double lo = L[(j + i) % M];
-            const double hi = U[((j - i) % M + M) % M];
+            const F lo = L[(j + i) % M];
+            const F hi = U[((j - i) % M + M) % M];
             out[i] = out[i] + (ANTI ? (lo - hi) : (lo + hi)) * wk;
         }
         L[j] = at(base - r + q + M);           // S_lo[q+M]   (slot of S_lo[q], done)
@@ -163,23 +136,24 @@ __device__ __forceinline__ void lds_pass(const double* __restrict__ s, int st, i
 // frames and keeps the centre — only the centre line is formed here).
 // Streaming, one voxel per lane; frames by stride (one stack) or pointer table.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, typename F>
 __global__ __launch_bounds__(256) void k_tderiv(Frames fr, long long fstride, size_t off0, size_t n, int rt,
-                                                const double* __restrict__ ht, double* __restrict__ D0) {
+                                                const F* __restrict__ ht, F* __restrict__ D0) {
     const size_t st = (size_t)gridDim.x * 256;
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) {
         const size_t idx = off0 + i;
-        double c, dt;
+        F c, dt;
         if (fstride) {
             const T* p = reinterpret_cast<const T*>(fr.p[0]) + idx;
-            c = (double)p[(long long)rt * fstride];
+            c = (F)p[(long long)rt * fstride];
             dt = c * ht[0];
             for (int k = rt; k >= 1; --k)
-                dt = dt + ((double)p[(long long)(rt - k) * fstride] - (double)p[(long long)(rt + k) * fstride]) * ht[k];
+                dt = dt + ((F)p[(long long)(rt - k) * fstride] - (F)p[(long long)(rt + k) * fstride]) * ht[k];
         } else {
-            c = ldf<T>(fr.p[rt], idx);
+            c = ldf<T, F>(fr.p[rt], idx);
             dt = c * ht[0];
-            for (int k = rt; k >= 1; --k) dt = dt + (ldf<T>(fr.p[rt - k], idx) - ldf<T>(fr.p[rt + k], idx)) * ht[k];
+            for (int k = rt; k >= 1; --k)
+                dt = dt + (ldf<T, F>(fr.p[rt - k], idx) - ldf<T, F>(fr.p[rt + k], idx)) * ht[k];
         }
         D0[i] = dt;
     }
@@ -194,8 +168,8 @@ struct K0Vec {
     static constexpr int B = V * (int)sizeof(T);  // 8 or 16 bytes
 };
 
-template <typename T>
-__device__ __forceinline__ void load_vec(const T* p, double (&v)[K0Vec<T>::V]) {
+template <typename T, typename F>
+__device__ __forceinline__ void load_vec(const T* p, F (&v)[K0Vec<T>::V]) {
     constexpr int V = K0Vec<T>::V;
     T t[V];
     if constexpr (K0Vec<T>::B == 8) {
@@ -206,30 +180,35 @@ __device__ __forceinline__ void load_vec(const T* p, double (&v)[K0Vec<T>::V]) {
         __builtin_memcpy(t, &raw, 16);
     }
 #pragma unroll
-    for (int i = 0; i < V; ++i) v[i] = (double)t[i];
+    for (int i = 0; i < V; ++i) v[i] = (F)t[i];
 }
 
-template <typename T>
+template <typename T, typename F>
 __global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size_t ngroups, int rt,
-                                                    const double* __restrict__ ht, double* __restrict__ D0) {
+                                                    const F* __restrict__ ht, F* __restrict__ D0) {
     constexpr int V = K0Vec<T>::V;
     const size_t st = (size_t)gridDim.x * 256;
     for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
         const size_t o = off0 + gi * V;
-        double c[V], a[V], b[V], dt[V];
-        load_vec<T>(reinterpret_cast<const T*>(fr.p[rt]) + o, c);
+        F c[V], a[V], b[V], dt[V];
+        load_vec<T, F>(reinterpret_cast<const T*>(fr.p[rt]) + o, c);
 #pragma unroll
         for (int i = 0; i < V; ++i) dt[i] = c[i] * ht[0];
         for (int k = rt; k >= 1; --k) {
-            load_vec<T>(reinterpret_cast<const T*>(fr.p[rt - k]) + o, a);
-            load_vec<T>(reinterpret_cast<const T*>(fr.p[rt + k]) + o, b);
-            const double w = ht[k];
+            load_vec<T, F>(reinterpret_cast<const T*>(fr.p[rt - k]) + o, a);
+            load_vec<T, F>(reinterpret_cast<const T*>(fr.p[rt + k]) + o, b);
+            const F w = ht[k];
 #pragma unroll
             for (int i = 0; i < V; ++i) dt[i] = dt[i] + (a[i] - b[i]) * w;
         }
-        double2* d = reinterpret_cast<double2*>(D0 + gi * V);
+        if constexpr (sizeof(F) == 8) {
+            double2* d = reinterpret_cast<double2*>(D0 + gi * V);
 #pragma unroll
-        for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
+            for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) D0[gi * V + i] = dt[i];
+        }
     }
 }
 
@@ -245,18 +224,19 @@ __global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size
 // ---------------------------------------------------------------------------
 constexpr int K1_R = 4, K1_TY = 4 * K1_R, K1_NZB = 4;
 
-template <typename T, int NJ>
-__global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, const double* __restrict__ D0, int ny,
-                                                 int nx, int nzp, DevTaps tp, double* __restrict__ B, size_t fs,
+template <typename T, typename F, int NJ>
+__global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
+                                                 int nx, int nzp, DevTaps<F> tp, F* __restrict__ B, size_t fs,
                                                  int need_b4) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* smem = reinterpret_cast<F*>(smem_raw);
     const int rd = tp.rd, rs = tp.rs;
     const int RH = K1_TY + 2 * rd;
-    double* sI = smem;
-    double* sT = sI + RH * 64;
-    double* sA1 = sT + RH * 64;
-    double* sA2 = sA1 + K1_TY * 64;
-    double* sA3 = sA2 + K1_TY * 64;
+    F* sI = smem;
+    F* sT = sI + RH * 64;
+    F* sA1 = sT + RH * 64;
+    F* sA2 = sA1 + K1_TY * 64;
+    F* sA3 = sA2 + K1_TY * 64;
     const int lane = threadIdx.x, w = threadIdx.y;
     const int x0 = blockIdx.x * (64 - 2 * rd), y0 = blockIdx.y * K1_TY;
     const int zb = blockIdx.z * K1_NZB;
@@ -266,14 +246,14 @@ __global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, co
     int roff[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) roff[j] = clampi(y0 - rd + w + 4 * j, 0, ny - 1) * nx + gx;
-    double rI[NJ], rT[NJ];
+    F rI[NJ], rT[NJ];
     auto fetch = [&](int t) {
         const T* ip = Ic + (size_t)(zb + t) * ps;
-        const double* dp = D0 + (size_t)(zb + t) * ps;
+        const F* dp = D0 + (size_t)(zb + t) * ps;
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
             if (w + 4 * j < RH) {
-                rI[j] = (double)ip[roff[j]];
+                rI[j] = (F)ip[roff[j]];
                 rT[j] = dp[roff[j]];
             }
     };
@@ -292,7 +272,7 @@ __global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, co
         __syncthreads();
         if (t + 1 < nzb) fetch(t + 1);
         {
-            double a[K1_R];
+            F a[K1_R];
             const int base = rd + w * K1_R;
             lds_pass<K1_R, false>(sT + lane, 64, base, tp.g, rd, a);
 #pragma unroll
@@ -306,14 +286,14 @@ __global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, co
         }
         __syncthreads();
         if (xout) {
-            double* bp = B + (size_t)(zb + t) * ps + gxo;
+            F* bp = B + (size_t)(zb + t) * ps + gxo;
 #pragma unroll
             for (int i = 0; i < K1_R; ++i) {
                 const int row = w * K1_R + i;
                 const int gy = y0 + row;
                 if (gy >= ny) break;
                 const int c = row * 64 + lane;
-                double b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
+                F b1 = sA1[c] * tp.g[0], b2 = sA2[c] * tp.s[0], b3 = sA3[c] * tp.d[0], b4 = sA3[c] * tp.s[0];
                 for (int k = rd; k >= 1; --k) {
                     b1 = b1 + (sA1[c - k] + sA1[c + k]) * tp.g[k];
                     b3 = b3 + (sA3[c - k] - sA3[c + k]) * tp.d[k];
@@ -341,12 +321,14 @@ __global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, co
 // ---------------------------------------------------------------------------
 constexpr int K2_R = 4, K2_ZC = 4 * K2_R;
 
-__global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, int zb0, double* __restrict__ G,
-                                                int zg0, int nzg, int nz, int ny, int nx, size_t fs, DevTaps tp) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+template <typename F>
+__global__ __launch_bounds__(256) void k_grad_z(const F* __restrict__ B, int zb0, F* __restrict__ G, int zg0, int nzg,
+                                                int nz, int ny, int nx, size_t fs, DevTaps<F> tp) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
     const int f = blockIdx.z & 3;
     const int zc = blockIdx.z >> 2;
-    const double* h = f == 0 ? tp.g : (f == 3 ? tp.d : tp.s);
+    const F* h = f == 0 ? tp.g : (f == 3 ? tp.d : tp.s);
     const int r = (f == 0 || f == 3) ? tp.rd : tp.rs;
     const int H = K2_ZC + 2 * r;
     const int lane = threadIdx.x, g = threadIdx.y;
@@ -355,17 +337,17 @@ __global__ __launch_bounds__(256) void k_grad_z(const double* __restrict__ B, in
     const int y = blockIdx.y;
     const int zc0 = zg0 + zc * K2_ZC;
     const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + xs;
-    const double* src = B + f * fs + col;
+    const F* src = B + f * fs + col;
     for (int row = g; row < H; row += 4)
         sm[row * 64 + lane] = src[(size_t)(clampi(zc0 - r + row, 0, nz - 1) - zb0) * ps];
     __syncthreads();
-    double out[K2_R];
+    F out[K2_R];
     if (f == 3)
         lds_pass<K2_R, true>(sm + lane, 64, r + g * K2_R, h, r, out);
     else
         lds_pass<K2_R, false>(sm + lane, 64, r + g * K2_R, h, r, out);
     if (x >= nx) return;
-    double* dst = G + f * fs + (size_t)y * nx + x;
+    F* dst = G + f * fs + (size_t)y * nx + x;
 #pragma unroll
     for (int i = 0; i < K2_R; ++i) {
         const int zl = zc0 + g * K2_R + i - zg0;
@@ -392,10 +374,11 @@ constexpr int K3_R = 8, K3_YC = 4 * K3_R;
 // next step's rows are fetched into registers during the current pass.
 constexpr int K3_STEP = K3_YC;
 
-template <int NP, int TJ>  // TJ >= ceil(2rw / 4): window rows each thread carries over
-__global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, double* __restrict__ P, int ny,
-                                                 int nx, size_t fs, const double* __restrict__ hw, int rw) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+template <typename F, int NP, int TJ>  // TJ >= ceil(2rw / 4): window rows each thread carries over
+__global__ __launch_bounds__(256) void k_prod_wy(const F* __restrict__ G, F* __restrict__ P, int ny, int nx,
+                                                 size_t fs, const F* __restrict__ hw, int rw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
     constexpr int NJ = K3_STEP / 4;  // new rows per thread per step
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
@@ -405,15 +388,15 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
     // packed product table (4 bits per entry)
     constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // a[] = {2,1,3,2,2,2,1,1,3} / {2,1,2,2,1}
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;  // b[] = {0,0,0,1,3,2,3,1,3} / {0,0,1,2,1}
-    const double* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
-    const double* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
+    const F* ga = G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl + xs;
+    const F* gb = G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl + xs;
     const int h2 = 2 * rw;
-    double* col = sm + lane;
+    F* col = sm + lane;
     for (int b = g; b < h2; b += 4) {  // prologue: y' in [0, 2rw)
         const size_t o = (size_t)clampi(b - rw, 0, ny - 1) * nx;
         col[b * 64] = ga[o] * gb[o];
     }
-    double ra[NJ], rb[NJ];
+    F ra[NJ], rb[NJ];
     auto fetch = [&](int yp0) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -423,15 +406,15 @@ __global__ __launch_bounds__(256) void k_prod_wy(const double* __restrict__ G, d
         }
     };
     fetch(h2);
-    double* o = P + p * fs + pl + x;
-    double tl[TJ];
+    F* o = P + p * fs + pl + x;
+    F tl[TJ];
     for (int y0 = 0; y0 < ny; y0 += K3_STEP) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) col[(h2 + g + 4 * j) * 64] = ra[j] * rb[j];
         __syncthreads();
         const bool more = y0 + K3_STEP < ny;
         if (more) fetch(y0 + K3_STEP + h2);
-        double out[K3_R];
+        F out[K3_R];
         lds_pass<K3_R, false>(col, 64, rw + g * K3_R, hw, rw, out);
         if (x < nx) {
 #pragma unroll
@@ -470,22 +453,22 @@ constexpr int K4_R = 8, K4_TX = 4 * K4_R, K4_ROWS = 64;
 // during the current pass.
 constexpr int k4_halo(int rw) { return (rw + 15) & ~15; }
 
-template <int NF, int TJ>  // TJ >= ceil(2ha / 32): tail column groups per loader lane
-__global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const double* __restrict__ P, double* __restrict__ Q,
-                                                             int ny, int nx, size_t fs,
-                                                             const double* __restrict__ hw, int rw) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+template <typename F, int NF, int TJ>  // TJ >= ceil(2ha / 32): tail column groups per loader lane
+__global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict__ P, F* __restrict__ Q, int ny,
+                                                             int nx, size_t fs, const F* __restrict__ hw, int rw) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
     const int ha = k4_halo(rw);
     const int h2 = 2 * ha;
     const int PP = (K4_TX + h2) | 1;
     constexpr int OP = K4_TX + 1;
-    double* so = sm + K4_ROWS * PP;  // output tile [row][K4_TX]
+    F* so = sm + K4_ROWS * PP;  // output tile [row][K4_TX]
     const int lane = threadIdx.x, g = threadIdx.y;
     const int y0 = blockIdx.y * K4_ROWS;
     const int f = blockIdx.z % NF;
     const size_t pl = (size_t)(blockIdx.z / NF) * ny * nx;
-    const double* src = P + f * fs + pl;
-    double* dst = Q + f * fs + pl;
+    const F* src = P + f * fs + pl;
+    F* dst = Q + f * fs + pl;
     // loader mapping: lanes 0..31 / 32..63 -> two rows, 32 consecutive columns
     const int lc = lane & 31, lr = (lane >> 5) + 2 * g;  // rows lr, lr + 8, ..., lr + 56
     int roff[8];  // row offsets (ny * nx < 2^31 per plan)
@@ -495,20 +478,20 @@ __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const double* __res
     for (int xp = lc; xp < h2; xp += 32)
 #pragma unroll
         for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + xp] = colv(j, xp);
-    double rv[8];
+    F rv[8];
     auto fetch = [&](int xp0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) rv[j] = colv(j, xp0 + lc);
     };
     fetch(h2);
-    double tl[TJ][8];
+    F tl[TJ][8];
     for (int x0 = 0; x0 < nx; x0 += K4_TX) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) sm[(lr + 8 * j) * PP + h2 + lc] = rv[j];
         __syncthreads();
         const bool more = x0 + K4_TX < nx;
         if (more) fetch(x0 + K4_TX + h2);
-        double out[K4_R];
+        F out[K4_R];
         lds_pass<K4_R, false>(sm + lane * PP, 1, ha + g * K4_R, hw, rw, out);
 #pragma unroll
         for (int i = 0; i < K4_R; ++i) so[lane * OP + g * K4_R + i] = out[i];
@@ -604,33 +587,36 @@ struct K5Geom {
 };
 constexpr K5Geom k5_geom(int rw) { return {rw <= 24 ? 8 : 4, 8}; }
 
-// Pointwise tail of K5: solve + reliability for the thread's R planes.
-template <typename RelT, int K5_R>
-__device__ __forceinline__ void k5_solve_store(const double (&acc)[9][K5_R], int z0l, int nzo, size_t o0, size_t ps,
-                                               double* __restrict__ vx, double* __restrict__ vy,
-                                               double* __restrict__ vz, RelT* __restrict__ rel) {
+// Pointwise tail of K5: solve + reliability for the thread's R planes, in
+// fp64 whatever the pass type F (fp32 plans solve their float tensor in fp64).
+template <typename F, typename RelT, int K5_R>
+__device__ __forceinline__ void k5_solve_store(const F (&acc)[9][K5_R], int z0l, int nzo, size_t o0, size_t ps,
+                                               F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
+                                               RelT* __restrict__ rel) {
 #pragma unroll
     for (int i = 0; i < K5_R; ++i) {
         if (z0l + i >= nzo) break;
         // field order: tx ty tz xy xz x2 yz y2 z2
+        const double tx = acc[0][i], ty = acc[1][i], tz = acc[2][i], xy = acc[3][i], xz = acc[4][i],
+                     x2 = acc[5][i], yz = acc[6][i], y2 = acc[7][i], z2 = acc[8][i];
         double ox, oy, oz;
-        solve3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i], acc[0][i], acc[1][i], acc[2][i], ox,
-               oy, oz);
+        solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
         const size_t o = (size_t)(z0l + i) * ps + o0;
-        vx[o] = ox;
-        vy[o] = oy;
-        vz[o] = oz;
-        rel[o] = (RelT)eigmin3(acc[5][i], acc[7][i], acc[8][i], acc[3][i], acc[4][i], acc[6][i]);
+        vx[o] = (F)ox;
+        vy[o] = (F)oy;
+        vz[o] = (F)oz;
+        rel[o] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
     }
 }
 
-template <typename RelT, int NJ, int K5_R, int K5_G>
-__global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict__ Q, int zq0, int nz, int ny, int nx,
-                                                  size_t fs, const double* __restrict__ hw, int rw, int zo0, int nzo,
-                                                  double* __restrict__ vx, double* __restrict__ vy,
-                                                  double* __restrict__ vz, RelT* __restrict__ rel) {
+template <typename F, typename RelT, int NJ, int K5_R, int K5_G>
+__global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
+                                                  size_t fs, const F* __restrict__ hw, int rw, int zo0, int nzo,
+                                                  F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
+                                                  RelT* __restrict__ rel) {
     constexpr int K5_ZC = K5_G * K5_R;
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
     const int H = K5_ZC + 2 * rw;
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
@@ -638,20 +624,20 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict
     const int y = blockIdx.y;
     const int zc0 = zo0 + blockIdx.z * K5_ZC;
     const size_t ps = (size_t)ny * nx, col = (size_t)y * nx + xs;
-    double rq[NJ];
+    F rq[NJ];
     auto fetch = [&](int f) {
-        const double* q = Q + f * fs + col;
+        const F* q = Q + f * fs + col;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int row = g + K5_G * j;
             if (row < H) rq[j] = q[(size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps];
         }
     };
-    double acc[9][K5_R];
+    F acc[9][K5_R];
     fetch(0);
 #pragma unroll
     for (int f = 0; f < 9; ++f) {
-        double* buf = sm + (f & 1) * H * 64;
+        F* buf = sm + (f & 1) * H * 64;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int row = g + K5_G * j;
@@ -662,7 +648,7 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const double* __restrict
         lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
     }
     if (x >= nx) return;
-    k5_solve_store<RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
+    k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
 // 16-byte global -> LDS copy (LDS-DMA): lane i's 16 bytes land at lds_byte + 16 i.
@@ -678,41 +664,45 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 
 // K5 with LDS-DMA staging: the field windows are loaded straight into NB LDS
 // buffers, NB - 1 fields ahead of the pass (no staging registers, no VGPR cost
-// for the prefetch), so a CU keeps up to (NB - 1) x 48 KB of loads in flight
-// instead of one field.  Lanes 0-31 / 32-63 of a wave load rows 2p / 2p+1 of
-// the window as 16-byte column pairs.  Needs nx even (16-byte aligned rows).
+// for the prefetch), so a CU keeps up to (NB - 1) windows of loads in flight
+// instead of one field.  One wave-instruction moves 64 lanes x 16 B = RPW rows
+// of the 64-column window (RPW = 2 for fp64, 4 for fp32).  Needs nx a
+// multiple of 16 B / sizeof(F) (16-byte aligned rows).
 // (A persistent form that also prefetches the next tile during the epilogue
 // spilled registers and measured slower.)
-template <typename RelT, int NJ2, int K5_R, int K5_G, int NB>
-__global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const double* __restrict__ Q, int zq0, int nz, int ny,
-                                                      int nx, size_t fs, const double* __restrict__ hw, int rw,
-                                                      int zo0, int nzo, double* __restrict__ vx,
-                                                      double* __restrict__ vy, double* __restrict__ vz,
+template <typename F, typename RelT, int NJ2, int K5_R, int K5_G, int NB>
+__global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
+                                                      size_t fs, const F* __restrict__ hw, int rw, int zo0, int nzo,
+                                                      F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
                                                       RelT* __restrict__ rel) {
     constexpr int K5_ZC = K5_G * K5_R;
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    constexpr int EPL = 16 / (int)sizeof(F);  // elements per lane per load
+    constexpr int RPW = EPL;                  // window rows per wave-instruction
+    constexpr int LPR = 64 / RPW;             // lanes per row
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
     const int H = K5_ZC + 2 * rw;
-    const int H2 = (H + 1) >> 1;  // row pairs per window
+    const int HG = (H + RPW - 1) / RPW;  // row groups per window
     const int lane = threadIdx.x, g = threadIdx.y;
     const int x = blockIdx.x * 64 + lane;
     const int y = blockIdx.y;
     const int zc0 = zo0 + blockIdx.z * K5_ZC;
     const size_t ps = (size_t)ny * nx;
-    const int xc = min((int)blockIdx.x * 64 + 2 * (lane & 31), nx - 2);  // this lane's column pair
-    const double* qrow = Q + (size_t)y * nx + xc;
-    const unsigned lds0 = (unsigned)(uintptr_t)sm;
+    const int xc = min((int)blockIdx.x * 64 + EPL * (lane % LPR), nx - EPL);  // this lane's columns
+    const F* qrow = Q + (size_t)y * nx + xc;
+    const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
     auto issue = [&](int f, int b) {
-        const double* q = qrow + f * fs;
-        const unsigned lb = lds0 + (unsigned)(b * H2 * 128 * sizeof(double));
+        const F* q = qrow + f * fs;
+        const unsigned lb = lds0 + (unsigned)(b * HG * 1024);
 #pragma unroll
         for (int j = 0; j < NJ2; ++j) {
-            const int p = min(g + K5_G * j, H2 - 1);  // surplus slots repeat the last pair: equal counts per wave
-            const int row = min(2 * p + (lane >> 5), H - 1);
-            const double* src = q + (size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps;
-            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(p * 128 * sizeof(double))));
+            const int p = min(g + K5_G * j, HG - 1);  // surplus slots repeat the last group: equal counts per wave
+            const int row = min(RPW * p + lane / LPR, H - 1);
+            const F* src = q + (size_t)(clampi(zc0 - rw + row, 0, nz - 1) - zq0) * ps;
+            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(p * 1024)));
         }
     };
-    double acc[9][K5_R];
+    F acc[9][K5_R];
 #pragma unroll
     for (int f = 0; f < NB - 1; ++f) issue(f, f);
 #pragma unroll
@@ -728,29 +718,29 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const double* __rest
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
-        lds_pass<K5_R, false>(sm + (f % NB) * H2 * 128 + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
+        lds_pass<K5_R, false>(sm + (f % NB) * HG * RPW * 64 + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
     }
     if (x >= nx) return;
-    k5_solve_store<RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
+    k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
-__global__ __launch_bounds__(256) void k_solve2d(const double* __restrict__ Q, size_t fs, int n,
-                                                 double* __restrict__ vx, double* __restrict__ vy,
-                                                 double* __restrict__ rel) {
+template <typename F>
+__global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t fs, int n, F* __restrict__ vx,
+                                                 F* __restrict__ vy, F* __restrict__ rel) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const double tx = Q[i], ty = Q[fs + i], xy = Q[2 * fs + i], x2 = Q[3 * fs + i], y2 = Q[4 * fs + i];
     const double det = (x2 * y2) - (xy * xy);
     const double R = 1.0 / (det + kEps);
-    vx[i] = R * ((y2 * -tx) + (-xy * -ty));
-    vy[i] = R * ((-xy * -tx) + (x2 * -ty));
+    vx[i] = (F)(R * ((y2 * -tx) + (-xy * -ty)));
+    vy[i] = (F)(R * ((-xy * -tx) + (x2 * -ty)));
     const double tr = x2 + y2;
     const double disc = tr * tr - 4.0 * det;
     const double L1 = (tr + sqrt(disc)) / 2.0;
     const double L2 = (tr - sqrt(disc)) / 2.0;
     // np.minimum propagates NaN
-    rel[i] = (L1 != L1) ? L1 : ((L2 != L2) ? L2 : (L1 < L2 ? L1 : L2));
+    rel[i] = (F)((L1 != L1) ? L1 : ((L2 != L2) ? L2 : (L1 < L2 ? L1 : L2)));
 }
 
 // ---------------------------------------------------------------------------
@@ -787,14 +777,16 @@ constexpr int kStages = 5;
 struct of3d_plan {
     int ndim = 3;
     bool rel64 = false;  // OF3D_REL_F64
+    bool fp32 = false;   // OF3D_FP32: passes in float
     int64_t nz = 1, ny = 1, nx = 1;
     int rd = 0, rs = 0, rt = 0, rw = 0;
     int device = 0;
     int64_t cap_planes = 0;  // planes per workspace field
     std::vector<double> htaps;  // host copy of half taps (g | d | s | t | w)
-    double* d_taps = nullptr;
-    double* X = nullptr;  // 9 fields
-    double* Y = nullptr;  // 9 fields
+    double* d_taps = nullptr;   // fp64 taps
+    float* d_taps32 = nullptr;  // the same rounded to float (OF3D_FP32)
+    void* X = nullptr;          // 9 fields of the pass type
+    void* Y = nullptr;          // 9 fields
     size_t fs = 0;        // field stride (elements)
     hipStream_t stream = nullptr;
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
@@ -844,9 +836,14 @@ int build_taps(const of3d_taps* t, of3d_plan* p) {
     return 0;
 }
 
-DevTaps dev_taps(const of3d_plan* p) {
-    DevTaps d;
-    const double* b = p->d_taps;
+template <typename F>
+DevTaps<F> dev_taps(const of3d_plan* p) {
+    DevTaps<F> d;
+    const F* b;
+    if constexpr (sizeof(F) == 8)
+        b = p->d_taps;
+    else
+        b = p->d_taps32;
     d.g = b;
     d.d = d.g + p->rd + 1;
     d.s = d.d + p->rd + 1;
@@ -861,35 +858,37 @@ DevTaps dev_taps(const of3d_plan* p) {
 
 unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
-template <typename T>
+template <typename T, typename F>
 const void* k1_kernel(int rd) {
     const int nj = (K1_TY + 2 * rd + 3) / 4;
-    if (nj <= 8) return (const void*)k_grad_xy<T, 8>;
-    if (nj <= 12) return (const void*)k_grad_xy<T, 12>;
-    return (const void*)k_grad_xy<T, 16>;
+    if (nj <= 8) return (const void*)k_grad_xy<T, F, 8>;
+    if (nj <= 12) return (const void*)k_grad_xy<T, F, 12>;
+    return (const void*)k_grad_xy<T, F, 16>;
 }
 
+template <typename F>
 const void* k1_kernel_dt(int dtype, int rd) {
     switch (dtype) {
-        case OF3D_U8: return k1_kernel<uint8_t>(rd);
-        case OF3D_U16: return k1_kernel<uint16_t>(rd);
-        case OF3D_I16: return k1_kernel<int16_t>(rd);
-        case OF3D_U32: return k1_kernel<uint32_t>(rd);
-        case OF3D_I32: return k1_kernel<int32_t>(rd);
-        case OF3D_F32: return k1_kernel<float>(rd);
-        default: return k1_kernel<double>(rd);
+        case OF3D_U8: return k1_kernel<uint8_t, F>(rd);
+        case OF3D_U16: return k1_kernel<uint16_t, F>(rd);
+        case OF3D_I16: return k1_kernel<int16_t, F>(rd);
+        case OF3D_U32: return k1_kernel<uint32_t, F>(rd);
+        case OF3D_I32: return k1_kernel<int32_t, F>(rd);
+        case OF3D_F32: return k1_kernel<float, F>(rd);
+        default: return k1_kernel<double, F>(rd);
     }
 }
 
+template <typename F>
 const void* k0v_kernel_dt(int dtype) {
     switch (dtype) {
-        case OF3D_U8: return (const void*)k_tderiv_vec<uint8_t>;
-        case OF3D_U16: return (const void*)k_tderiv_vec<uint16_t>;
-        case OF3D_I16: return (const void*)k_tderiv_vec<int16_t>;
-        case OF3D_U32: return (const void*)k_tderiv_vec<uint32_t>;
-        case OF3D_I32: return (const void*)k_tderiv_vec<int32_t>;
-        case OF3D_F32: return (const void*)k_tderiv_vec<float>;
-        default: return (const void*)k_tderiv_vec<double>;
+        case OF3D_U8: return (const void*)k_tderiv_vec<uint8_t, F>;
+        case OF3D_U16: return (const void*)k_tderiv_vec<uint16_t, F>;
+        case OF3D_I16: return (const void*)k_tderiv_vec<int16_t, F>;
+        case OF3D_U32: return (const void*)k_tderiv_vec<uint32_t, F>;
+        case OF3D_I32: return (const void*)k_tderiv_vec<int32_t, F>;
+        case OF3D_F32: return (const void*)k_tderiv_vec<float, F>;
+        default: return (const void*)k_tderiv_vec<double, F>;
     }
 }
 
@@ -898,79 +897,97 @@ int k0_vec_width(int dtype) {
     return es == 1 ? 8 : (es == 8 ? 2 : 4);
 }
 
+template <typename F>
 const void* k0_kernel_dt(int dtype) {
     switch (dtype) {
-        case OF3D_U8: return (const void*)k_tderiv<uint8_t>;
-        case OF3D_U16: return (const void*)k_tderiv<uint16_t>;
-        case OF3D_I16: return (const void*)k_tderiv<int16_t>;
-        case OF3D_U32: return (const void*)k_tderiv<uint32_t>;
-        case OF3D_I32: return (const void*)k_tderiv<int32_t>;
-        case OF3D_F32: return (const void*)k_tderiv<float>;
-        default: return (const void*)k_tderiv<double>;
+        case OF3D_U8: return (const void*)k_tderiv<uint8_t, F>;
+        case OF3D_U16: return (const void*)k_tderiv<uint16_t, F>;
+        case OF3D_I16: return (const void*)k_tderiv<int16_t, F>;
+        case OF3D_U32: return (const void*)k_tderiv<uint32_t, F>;
+        case OF3D_I32: return (const void*)k_tderiv<int32_t, F>;
+        case OF3D_F32: return (const void*)k_tderiv<float, F>;
+        default: return (const void*)k_tderiv<double, F>;
     }
 }
 
-template <typename RelT>
+template <typename F, typename RelT>
 const void* k5_kernel(int rw) {
     // NJ = rows per thread of the staged window: ceil((G * R + 2rw) / G)
     const K5Geom k = k5_geom(rw);
-    if (k.r == 8) return rw <= 16 ? (const void*)k_wz_solve<RelT, 12, 8, 8> : (const void*)k_wz_solve<RelT, 14, 8, 8>;
+    if (k.r == 8)
+        return rw <= 16 ? (const void*)k_wz_solve<F, RelT, 12, 8, 8> : (const void*)k_wz_solve<F, RelT, 14, 8, 8>;
     const int nj = (8 * 4 + 2 * rw + 7) / 8;
     switch (nj <= 10 ? 10 : (nj <= 12 ? 12 : 16)) {
-        case 10: return (const void*)k_wz_solve<RelT, 10, 4, 8>;
-        case 12: return (const void*)k_wz_solve<RelT, 12, 4, 8>;
-        default: return (const void*)k_wz_solve<RelT, 16, 4, 8>;
+        case 10: return (const void*)k_wz_solve<F, RelT, 10, 4, 8>;
+        case 12: return (const void*)k_wz_solve<F, RelT, 12, 4, 8>;
+        default: return (const void*)k_wz_solve<F, RelT, 16, 4, 8>;
     }
 }
 
-// LDS-DMA K5: NB window buffers of ceil(H / 2) row pairs; NJ2 = pairs per wave.
+// LDS-DMA K5: NB window buffers of ceil(H / RPW) 1-KB row groups (RPW = 16 B /
+// sizeof(F) rows); NJ2 = groups per wave.
 #ifndef OF3D_K5_DMA
 #define OF3D_K5_DMA 1
 #endif
-constexpr int k5_pairs(int rw) { return (k5_geom(rw).g * k5_geom(rw).r + 2 * rw + 1) / 2; }
+template <typename F>
+constexpr int k5_groups(int rw) {
+    constexpr int rpw = 16 / (int)sizeof(F);
+    return (k5_geom(rw).g * k5_geom(rw).r + 2 * rw + rpw - 1) / rpw;
+}
+template <typename F>
 int k5_dma_nb(int rw) {
     if (!OF3D_K5_DMA) return 0;
-    const size_t buf = (size_t)k5_pairs(rw) * 128 * sizeof(double), lim = 160 * 1024;
+    const size_t buf = (size_t)k5_groups<F>(rw) * 1024, lim = 160 * 1024;
     return 3 * buf <= lim ? 3 : (2 * buf <= lim ? 2 : 0);
 }
 
-template <typename RelT>
+template <typename F, typename RelT>
 const void* k5_dma_kernel(int rw, int nb) {
     const K5Geom k = k5_geom(rw);
-    const int nj2 = (k5_pairs(rw) + k.g - 1) / k.g;
-#define OF3D_K5D(NJ2, R) \
-    (nb == 3 ? (const void*)k_wz_solve_dma<RelT, NJ2, R, 8, 3> : (const void*)k_wz_solve_dma<RelT, NJ2, R, 8, 2>)
-    if (k.r == 8) return nj2 <= 6 ? OF3D_K5D(6, 8) : OF3D_K5D(7, 8);  // rw <= 24: nj2 <= 7
-    return nj2 <= 6 ? OF3D_K5D(6, 4) : (nj2 <= 7 ? OF3D_K5D(7, 4) : OF3D_K5D(8, 4));  // rw <= 48: nj2 <= 8
+    const int nj2 = (k5_groups<F>(rw) + k.g - 1) / k.g;
+#define OF3D_K5D(NJ2, R)                                                     \
+    (nb == 3 ? (const void*)k_wz_solve_dma<F, RelT, NJ2, R, 8, 3>            \
+             : (const void*)k_wz_solve_dma<F, RelT, NJ2, R, 8, 2>)
+    if constexpr (sizeof(F) == 8) {
+        if (k.r == 8) return nj2 <= 6 ? OF3D_K5D(6, 8) : OF3D_K5D(7, 8);  // rw <= 24: nj2 <= 7
+        return nj2 <= 6 ? OF3D_K5D(6, 4) : (nj2 <= 7 ? OF3D_K5D(7, 4) : OF3D_K5D(8, 4));  // rw <= 48: nj2 <= 8
+    } else {
+        if (k.r == 8) return nj2 <= 3 ? OF3D_K5D(3, 8) : OF3D_K5D(4, 8);  // rw <= 24: nj2 <= 4
+        return nj2 <= 3 ? OF3D_K5D(3, 4) : OF3D_K5D(4, 4);                // rw <= 48: nj2 <= 4
+    }
 #undef OF3D_K5D
 }
 
+template <typename F>
 const void* k3_kernel(int np, int rw) {
     const int tj = (2 * rw + 3) / 4;  // <= 24 for rw <= 48
     if (np == 9) {
-        if (tj <= 8) return (const void*)k_prod_wy<9, 8>;
-        if (tj <= 12) return (const void*)k_prod_wy<9, 12>;
-        return (const void*)k_prod_wy<9, 24>;
+        if (tj <= 8) return (const void*)k_prod_wy<F, 9, 8>;
+        if (tj <= 12) return (const void*)k_prod_wy<F, 9, 12>;
+        return (const void*)k_prod_wy<F, 9, 24>;
     }
-    if (tj <= 8) return (const void*)k_prod_wy<5, 8>;
-    if (tj <= 12) return (const void*)k_prod_wy<5, 12>;
-    return (const void*)k_prod_wy<5, 24>;
+    if (tj <= 8) return (const void*)k_prod_wy<F, 5, 8>;
+    if (tj <= 12) return (const void*)k_prod_wy<F, 5, 12>;
+    return (const void*)k_prod_wy<F, 5, 24>;
 }
 
+template <typename F>
 const void* k4_kernel(int nf, int rw) {
     const int tj = (2 * k4_halo(rw) + 31) / 32;  // <= 3 for rw <= 48
-    if (nf == 9) return tj <= 1 ? (const void*)k_wx<9, 1> : (tj == 2 ? (const void*)k_wx<9, 2> : (const void*)k_wx<9, 3>);
-    return tj <= 1 ? (const void*)k_wx<5, 1> : (tj == 2 ? (const void*)k_wx<5, 2> : (const void*)k_wx<5, 3>);
+    if (nf == 9)
+        return tj <= 1 ? (const void*)k_wx<F, 9, 1>
+                       : (tj == 2 ? (const void*)k_wx<F, 9, 2> : (const void*)k_wx<F, 9, 3>);
+    return tj <= 1 ? (const void*)k_wx<F, 5, 1> : (tj == 2 ? (const void*)k_wx<F, 5, 2> : (const void*)k_wx<F, 5, 3>);
 }
 
-int set_attrs(of3d_plan* p) {
-    if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
-
-    p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * sizeof(double);
-    p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * sizeof(double);
-    p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * sizeof(double);
-    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * sizeof(double);
-    p->k5_lds = (size_t)2 * (k5_geom(p->rw).g * k5_geom(p->rw).r + 2 * p->rw) * 64 * sizeof(double);
+template <typename F>
+int set_attrs_t(of3d_plan* p) {
+    const size_t e = sizeof(F);
+    p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * e;
+    p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * e;
+    p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * e;
+    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * e;
+    p->k5_lds = (size_t)2 * (k5_geom(p->rw).g * k5_geom(p->rw).r + 2 * p->rw) * 64 * e;
     const size_t lim = 160 * 1024;
     if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
     auto attr = [&](const void* k, size_t b) -> int {
@@ -978,18 +995,24 @@ int set_attrs(of3d_plan* p) {
         return 0;
     };
     int rc = 0;
-    for (int dt = OF3D_U8; dt <= OF3D_F64; ++dt) rc |= attr(k1_kernel_dt(dt, p->rd), p->k1_lds);
-    rc |= attr((const void*)k_grad_z, p->k2_lds);
-    rc |= attr(k3_kernel(9, p->rw), p->k3_lds) | attr(k3_kernel(5, p->rw), p->k3_lds);
-    rc |= attr(k4_kernel(9, p->rw), p->k4_lds) | attr(k4_kernel(5, p->rw), p->k4_lds);
-    rc |= attr(k5_kernel<float>(p->rw), p->k5_lds) | attr(k5_kernel<double>(p->rw), p->k5_lds);
-    p->k5_nb = (p->nx % 2 == 0 && p->nx >= 2) ? k5_dma_nb(p->rw) : 0;
+    for (int dt = OF3D_U8; dt <= OF3D_F64; ++dt) rc |= attr(k1_kernel_dt<F>(dt, p->rd), p->k1_lds);
+    rc |= attr((const void*)k_grad_z<F>, p->k2_lds);
+    rc |= attr(k3_kernel<F>(9, p->rw), p->k3_lds) | attr(k3_kernel<F>(5, p->rw), p->k3_lds);
+    rc |= attr(k4_kernel<F>(9, p->rw), p->k4_lds) | attr(k4_kernel<F>(5, p->rw), p->k4_lds);
+    rc |= attr(k5_kernel<F, float>(p->rw), p->k5_lds) | attr(k5_kernel<F, double>(p->rw), p->k5_lds);
+    constexpr int epl = 16 / (int)sizeof(F);
+    p->k5_nb = (p->nx % epl == 0) ? k5_dma_nb<F>(p->rw) : 0;
     if (p->k5_nb) {
-        p->k5d_lds = (size_t)p->k5_nb * k5_pairs(p->rw) * 128 * sizeof(double);
-        rc |= attr(k5_dma_kernel<float>(p->rw, p->k5_nb), p->k5d_lds) |
-              attr(k5_dma_kernel<double>(p->rw, p->k5_nb), p->k5d_lds);
+        p->k5d_lds = (size_t)p->k5_nb * k5_groups<F>(p->rw) * 1024;
+        rc |= attr(k5_dma_kernel<F, float>(p->rw, p->k5_nb), p->k5d_lds) |
+              attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
     }
     return rc ? -1 : 0;
+}
+
+int set_attrs(of3d_plan* p) {
+    if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
+    return p->fp32 ? set_attrs_t<float>(p) : set_attrs_t<double>(p);
 }
 
 struct Ranges {
@@ -1012,8 +1035,14 @@ Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
     return r;
 }
 
-int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, double* vx,
-        double* vy, double* vz, void* rel, hipStream_t s) {
+template <typename F>
+int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx_,
+          void* vy_, void* vz_, void* rel, hipStream_t s) {
+    F* vx = (F*)vx_;
+    F* vy = (F*)vy_;
+    F* vz = (F*)vz_;
+    F* X = (F*)p->X;
+    F* Y = (F*)p->Y;
     if (!p) return fail("of3d: null plan");
     if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
     const Ranges R = ranges(p, zo0, zo1);
@@ -1026,7 +1055,7 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         if (!d_frames[i]) return fail("of3d: null frame pointer");
         fr.p[i] = d_frames[i];
     }
-    const DevTaps tp = dev_taps(p);
+    const DevTaps<F> tp = dev_taps<F>(p);
     const size_t fs = p->fs;
     const int nb = (int)(R.zb1 - R.zb0), ng = (int)(R.zg1 - R.zg0), no = (int)(R.zo1 - R.zo0);
     hipEvent_t* evs = p->host_ev ? p->ev
@@ -1050,7 +1079,7 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
         const size_t plane = (size_t)ny * nx;
         size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)nb * plane;
         int rt_arg = p->rt;
-        double* D0 = p->Y;  // Y field 0 is free until K2 writes it
+        F* D0 = Y;  // Y field 0 is free until K2 writes it
         const int V = k0_vec_width(dtype);
         const size_t vb = (size_t)V * es;
         bool vec = off0 % V == 0 && n % V == 0;
@@ -1059,70 +1088,70 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
             size_t ng = n / V;
             const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
             void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0v_kernel_dt(dtype), dim3(blocks), dim3(256), args, 0, s));
+            OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
         } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
             void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
                             (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0_kernel_dt(dtype), dim3(blocks), dim3(256), args, 0, s));
+            OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
         }
         {
             const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
-            const double* D0c = D0;
+            const F* D0c = D0;
             int need_b4 = p->ndim == 3, nb_arg = nb;
             dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
             void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
-                            (void*)&p->X, (void*)&fs, (void*)&need_b4};
-            OF3D_HIP(hipLaunchKernel(k1_kernel_dt(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
+                            (void*)&X, (void*)&fs, (void*)&need_b4};
+            OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
         }
     }
     OF3D_MARK(1);
-    const double* G;
+    const F* G;
     if (p->ndim == 3) {
         dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
-        hipLaunchKernelGGL(k_grad_z, g, dim3(64, 4), p->k2_lds, s, p->X, (int)R.zb0, p->Y, (int)R.zg0, ng, nz, ny, nx,
-                           fs, tp);
+        hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, s, X, (int)R.zb0, Y, (int)R.zg0, ng, nz, ny, nx, fs,
+                           tp);
         OF3D_HIP(hipGetLastError());
-        G = p->Y;
+        G = Y;
     } else {
-        G = p->X;
+        G = X;
     }
     OF3D_MARK(2);
-    double* P = p->ndim == 3 ? p->X : p->Y;
-    double* Q = p->ndim == 3 ? p->Y : p->X;
+    F* P = p->ndim == 3 ? X : Y;
+    F* Q = p->ndim == 3 ? Y : X;
     const int nf = p->ndim == 3 ? 9 : 5;
     {
         dim3 g(cdiv(nx, 64), 1, ng * nf);
         int rw_arg = p->rw;
         void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k3_kernel(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
+        OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
     }
     OF3D_MARK(3);
     {
         dim3 g(1, cdiv(ny, K4_ROWS), ng * nf);
         int rw_arg = p->rw;
-        const double* Pc = P;
+        const F* Pc = P;
         void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k4_kernel(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
+        OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {
         const K5Geom kg = k5_geom(p->rw);
         dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
         int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
-        const double* Qc = Q;
+        const F* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
         if (p->k5_nb) {
-            const void* k5 = p->rel64 ? k5_dma_kernel<double>(p->rw, p->k5_nb) : k5_dma_kernel<float>(p->rw, p->k5_nb);
+            const void* k5 = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
             OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
         } else {
-            const void* k5 = p->rel64 ? k5_kernel<double>(p->rw) : k5_kernel<float>(p->rw);
+            const void* k5 = p->rel64 ? k5_kernel<F, double>(p->rw) : k5_kernel<F, float>(p->rw);
             OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5_lds, s));
         }
     } else {
         const int n = ny * nx;
-        hipLaunchKernelGGL(k_solve2d, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (double*)rel);
+        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (F*)rel);
     }
     OF3D_HIP(hipGetLastError());
     OF3D_MARK(5);
@@ -1132,11 +1161,17 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
     return 0;
 }
 
+int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx,
+        void* vy, void* vz, void* rel, hipStream_t s) {
+    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s)
+                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
+}
+
 int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
                 int device, int64_t max_out_planes) {
     if (!out) return fail("of3d: null plan pointer");
     *out = nullptr;
-    if ((mode & ~OF3D_REL_F64) != OF3D_FP64_EXACT) return fail("of3d: unsupported mode");
+    if ((mode & ~(OF3D_REL_F64 | OF3D_FP32)) != OF3D_FP64_EXACT) return fail("of3d: unsupported mode");
     if (ndim != 2 && ndim != 3) return fail("of3d: ndim must be 2 or 3");
     if (ndim == 2 && nz != 1) return fail("of3d: 2D plans need nz == 1");
     if (nz < 1 || ny < 1 || nx < 1) return fail("of3d: empty volume");
@@ -1144,6 +1179,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     std::unique_ptr<of3d_plan> p(new of3d_plan);
     p->ndim = ndim;
     p->rel64 = (mode & OF3D_REL_F64) != 0;
+    p->fp32 = (mode & OF3D_FP32) != 0;
     p->nz = nz;
     p->ny = ny;
     p->nx = nx;
@@ -1156,8 +1192,14 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->fs = (size_t)p->cap_planes * ny * nx;
     OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
     OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
-    OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * sizeof(double)));
-    OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * sizeof(double)));
+    {
+        std::vector<float> h32(p->htaps.begin(), p->htaps.end());  // round-to-nearest, as numpy's astype
+        OF3D_HIP(hipMalloc(&p->d_taps32, h32.size() * sizeof(float)));
+        OF3D_HIP(hipMemcpy(p->d_taps32, h32.data(), h32.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+    const size_t es = p->fp32 ? sizeof(float) : sizeof(double);
+    OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * es));
+    OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * es));
     OF3D_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     for (auto& e : p->ev) OF3D_HIP(hipEventCreate(&e));
     *out = p.release();
@@ -1169,6 +1211,7 @@ void plan_free(of3d_plan* p) {
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     (void)hipFree(p->d_taps);
+    (void)hipFree(p->d_taps32);
     (void)hipFree(p->X);
     (void)hipFree(p->Y);
     (void)hipFree(p->d_in);
@@ -1216,6 +1259,7 @@ int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, i
     const auto t0 = std::chrono::steady_clock::now();
     if (!images || !vx || !vy || !rel || (ndim == 3 && !vz)) return fail("of3d: null buffer");
     if (!taps) return fail("of3d: null taps");
+    if (mode & OF3D_FP32) return fail("of3d: OF3D_FP32 is a plan mode (float outputs); use of3d_plan_*");
     const size_t es = dtype_size(dtype);
     if (!es) return fail("of3d: unsupported dtype");
     if (nt < 1 || !(nt & 1)) return fail("of3d: nt must be odd");
@@ -1367,7 +1411,9 @@ int of3d_plan_destroy(of3d_plan* plan) {
     return 0;
 }
 
-size_t of3d_plan_workspace_bytes(const of3d_plan* p) { return p ? 18 * p->fs * sizeof(double) : 0; }
+size_t of3d_plan_workspace_bytes(const of3d_plan* p) {
+    return p ? 18 * p->fs * (p->fp32 ? sizeof(float) : sizeof(double)) : 0;
+}
 
 int of3d_plan_input_range(const of3d_plan* p, int64_t zo0, int64_t zo1, int64_t* zi0, int64_t* zi1) {
     if (!p || !zi0 || !zi1) return fail("of3d: null argument");
@@ -1379,7 +1425,7 @@ int of3d_plan_input_range(const of3d_plan* p, int64_t zo0, int64_t zo1, int64_t*
 }
 
 int of3d_plan_execute(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1,
-                      double* vx, double* vy, double* vz, void* rel, void* stream) {
+                      void* vx, void* vy, void* vz, void* rel, void* stream) {
     if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
     OF3D_HIP(hipSetDevice(p->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->stream;

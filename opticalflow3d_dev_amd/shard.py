@@ -107,12 +107,12 @@ class SlabRunner:
 
     frames: uint16/... device tensor (2*rt+1, zi1-zi0, Ny, Nx) holding planes [zi0, zi1)."""
 
-    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=0, timing=0):
+    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=0, timing=0, mode=0):
         self.nz, self.ny, self.nx = nz, ny, nx
         self.z0, self.z1 = z0, z1
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.plan = _lib.Plan(3, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=device,
-                              max_out_planes=max(z1 - z0, 1), timing=timing)
+                              max_out_planes=max(z1 - z0, 1), timing=timing, mode=mode)
         self.zi0, self.zi1 = self.plan.input_range(z0, z1)
 
     def run(self, frames, dtype_code, vx, vy, vz, rel, stream=0):
@@ -132,6 +132,8 @@ def fill_halos(block, zi0: int, z0: int, z1: int, nz: int, halo: int, rank: int,
     import torch
     import torch.distributed as dist
 
+    if world == 1:
+        return block
     zi1 = zi0 + block.shape[-3]
     # gloo moves host tensors only: stage CUDA planes through host memory there
     stage = block.is_cuda and dist.get_backend(group) == "gloo"
@@ -174,14 +176,14 @@ class ZSlabFlow:
     planes [z0, z1) — bit-identical to the unsharded frame.  Outputs stay on
     this rank (no gather)."""
 
-    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, rank, world, device=0, timing=0, group=None):
+    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, rank, world, device=0, timing=0, group=None, mode=0):
         self.rank, self.world, self.group = rank, world, group
         self.z0, self.z1 = zslab_bounds(nz, rank, world)
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.halo = self.rd + self.rw
         self.nz, self.ny, self.nx = nz, ny, nx
-        self.runner = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, self.z0, self.z1, device=device, timing=timing) \
-            if self.z1 > self.z0 else None
+        self.runner = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, self.z0, self.z1, device=device, timing=timing,
+                                 mode=mode) if self.z1 > self.z0 else None
         self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw)
         if self.runner is not None:
             assert (self.runner.zi0, self.runner.zi1) == (self.zi0, self.zi1)

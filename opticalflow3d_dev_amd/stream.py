@@ -47,7 +47,7 @@ class FlowStream:
     .release() hands the buffer set back (at most `depth` frames in flight)."""
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
-                 d2h_blocks=64):
+                 d2h_blocks=64, precision="fp64"):
         import torch
 
         self.torch = torch
@@ -68,7 +68,11 @@ class FlowStream:
         self.nvox = nz * ny * nx
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.nwin = 2 * self.rt + 1
-        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device)
+        if precision not in ("fp64", "fp32"):
+            raise ValueError("precision must be 'fp64' (bit-exact) or 'fp32'")
+        self.precision = precision
+        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device,
+                              mode=_lib.OF3D_FP32 if precision == "fp32" else 0)
         self.ring = torch.empty((self.nwin, self.nvox), dtype=tdt, device=self.dev)
         self.order = []  # ring slots of the resident frames, oldest first
         self.free = list(range(self.nwin))
@@ -100,10 +104,11 @@ class FlowStream:
             self.dl_thread = threading.Thread(target=self._download_loop, daemon=True)
             self.dl_thread.start()
         nout = 4 if ndim == 3 else 3
-        rel_t = torch.float32 if ndim == 3 else torch.float64
+        v_t = torch.float32 if precision == "fp32" else torch.float64
+        rel_t = torch.float32 if (ndim == 3 or precision == "fp32") else torch.float64
         self.depth = depth
         self.d2h_blocks = d2h_blocks
-        mk = lambda pin: [torch.empty(self.nvox, dtype=torch.float64, device=None if pin else self.dev,
+        mk = lambda pin: [torch.empty(self.nvox, dtype=v_t, device=None if pin else self.dev,
                                       pin_memory=pin) for _ in range(nout - 1)] + \
                          [torch.empty(self.nvox, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
         self.dout = [mk(False) for _ in range(depth)]
