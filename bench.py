@@ -177,13 +177,51 @@ def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
             "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
 
 
-def roofline(stages, model, cfg, frame_bytes, nwin, sv=8):
-    """roofline object of the bench line: the dominant stage (HIP-event average over the timed
-    region) against HBM peak, with its PMC traffic, plus the whole-frame figure."""
-    dom = max(stages, key=stages.get)
-    dom_ms = stages[dom]
+def timed_region(step, plan, args, world, dev):
+    """warmup -> stage profile (K steps with all five stages timed, outside the timed
+    region: every HIP event is a barrier packet between kernels, so timing all stages
+    inflates the frame by ~8 %) -> the timed region: K steps bracketed by barrier +
+    synchronize, with HIP events only around the dominant stage (the roofline kernel).
+    Returns (elapsed_s, stage profile ms, dominant stage, its ms inside the timed region)."""
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    profile, dom, dom_ms = {}, None, None
+    if plan is not None:
+        try:
+            plan.stage_times()  # drop warmup records
+        except RuntimeError:
+            pass
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        profile = plan.stage_times()
+        dom = max(profile, key=profile.get)
+        plan.set_timing_stages([dom])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if plan is not None:
+        dom_ms = plan.stage_times()[dom]
+    return elapsed, profile, dom, dom_ms
+
+
+def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, nwin, sv=8):
+    """roofline object of the bench line: the dominant stage, its HIP-event average over the
+    timed region, against HBM peak, with its PMC traffic; plus the per-stage profile and the
+    whole-frame figure."""
     ach = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
-    frame_ms = sum(stages.values())
+    frame_ms = sum(profile.values())
     return {
         "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, cfg),
@@ -191,7 +229,8 @@ def roofline(stages, model, cfg, frame_bytes, nwin, sv=8):
         "valu_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
         "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 /
                            (FP64_VALU_PEAK_TOPS if sv == 8 else FP32_VALU_PEAK_TOPS), 4),
-        "stage_ms": {k: round(v, 5) for k, v in stages.items()},
+        "stage_ms": {k: round(v, 5) for k, v in profile.items()},
+        "stage_ms_note": "separate profile pass with events at every stage boundary (adds ~5 us per event)",
         "frame": {"bytes_per_voxel": nwin * 2 + 3 * sv + 4, "device_ms": round(frame_ms, 4),
                   "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
                   "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
@@ -225,25 +264,8 @@ def run_zslab(args, world, rank, local_rank, dev):
     def step():
         zf.run(_lib.OF3D_U16, *outs, rel, stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if zf.runner is not None:
-        try:
-            zf.runner.plan.stage_times()
-        except RuntimeError:
-            pass
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stages = zf.runner.plan.stage_times() if zf.runner is not None else {}
+    elapsed, profile, dom, dom_ms = timed_region(step, zf.runner.plan if zf.runner is not None else None, args,
+                                                 world, dev)
     finite = bool(torch.isfinite(outs[0][:n_out]).all().item()) if n_out else True
     if world > 1:
         tt = torch.tensor([elapsed, 0.0 if finite else 1.0], dtype=torch.float64, device=dev)
@@ -254,8 +276,8 @@ def run_zslab(args, world, rank, local_rank, dev):
         nb, no = zf.zi1 - zf.zi0, zf.z1 - zf.z0
         ng = min(zf.z1 + rw, nz) - max(zf.z0 - rw, 0)
         sv = 4 if fp32 else 8
-        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx, sv), args.config,
-                        (nwin * 2 + 3 * sv + 4) * no * ny * nx, nwin, sv)
+        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx, sv),
+                        args.config, (nwin * 2 + 3 * sv + 4) * no * ny * nx, nwin, sv)
         roof["frame"]["note"] = "rank 0's slab (output planes %d..%d, input planes %d..%d)" % (
             zf.z0, zf.z1, zf.zi0, zf.zi1)
         cpu = None
@@ -336,24 +358,7 @@ def main():
         plan.execute(fptrs, _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(), d_vz.data_ptr(),
                      d_rel.data_ptr(), stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    try:
-        plan.stage_times()  # drop warmup records
-    except RuntimeError:
-        pass
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    stages = plan.stage_times()
+    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -365,7 +370,7 @@ def main():
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         value = world * vox * args.steps / elapsed / 1e6
-        roof = roofline(stages, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
+        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
                         args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox, nwin, sv)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

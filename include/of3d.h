@@ -144,8 +144,13 @@ int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, i
  * of3d_plan_stage_times: average device time (ms) per stage over the
  * executions recorded since the previous read (at most `slots`), then reset;
  * returns the number of stages written (<= cap).  Stage names:
- * of3d_stage_name(i) = grad_xy, grad_z, prod_wy, wx, wz_solve. */
+ * of3d_stage_name(i) = grad_xy, grad_z, prod_wy, wx, wz_solve.
+ * of3d_plan_set_timing_mask(plan, mask): time only the stages in the bit
+ * mask (bit i = stage i; default all).  Each event is a barrier packet
+ * between two kernels, so fewer events perturb the pipeline less; stages
+ * outside the mask read back as -1. */
 int of3d_plan_set_timing(of3d_plan* plan, int slots);
+int of3d_plan_set_timing_mask(of3d_plan* plan, unsigned mask);
 int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
 const char* of3d_stage_name(int i);
 

@@ -36,7 +36,7 @@ EXPORTED = (
     "of3d_version", "of3d_last_error", "of3d_device_count", "of3d_flow3d", "of3d_flow2d",
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
-    "of3d_copy_async", "of3d_dma_copy",
+    "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask",
 )
 
 
@@ -111,6 +111,8 @@ def load():
         lib.of3d_stage_name.restype = ctypes.c_char_p
         lib.of3d_plan_set_timing.argtypes = [P, ctypes.c_int]
         lib.of3d_plan_set_timing.restype = ctypes.c_int
+        lib.of3d_plan_set_timing_mask.argtypes = [P, ctypes.c_uint]
+        lib.of3d_plan_set_timing_mask.restype = ctypes.c_int
         lib.of3d_copy_async.argtypes = [P, P, ctypes.c_size_t, ctypes.c_int, P]
         lib.of3d_copy_async.restype = ctypes.c_int
         lib.of3d_dma_copy.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
@@ -194,7 +196,16 @@ class Plan:
     def stage_times(self):
         buf = (ctypes.c_double * 8)()
         n = check(self.lib.of3d_plan_stage_times(self.handle, buf, 8))
-        return {self.lib.of3d_stage_name(i).decode(): buf[i] for i in range(n)}
+        return {self.lib.of3d_stage_name(i).decode(): buf[i] for i in range(n) if buf[i] >= 0}
+
+    STAGES = ("grad_xy", "grad_z", "prod_wy", "wx", "wz_solve")
+
+    def set_timing_stages(self, names=None):
+        """Time only these stages (None: all); fewer events, less perturbation."""
+        mask = 0
+        for n in (names or self.STAGES):
+            mask |= 1 << self.STAGES.index(n)
+        check(self.lib.of3d_plan_set_timing_mask(self.handle, mask))
 
     def close(self):
         if getattr(self, "handle", None):

@@ -224,8 +224,11 @@ __global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size
 // ---------------------------------------------------------------------------
 constexpr int K1_R = 4, K1_TY = 4 * K1_R, K1_NZB = 4;
 
+#ifndef OF3D_K1_OCC
+#define OF3D_K1_OCC 3
+#endif
 template <typename T, typename F, int NJ>
-__global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
+__global__ __launch_bounds__(256, OF3D_K1_OCC) void k_grad_xy(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
                                                  int nx, int nzp, DevTaps<F> tp, F* __restrict__ B, size_t fs,
                                                  int need_b4) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -795,6 +798,7 @@ struct of3d_plan {
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
+    unsigned timing_mask = (1u << kStages) - 1;  // stages timed (events at their two boundaries)
     std::vector<hipEvent_t> tev;     // timing_slots * (kStages + 1)
     int64_t tcount = 0;              // executions recorded since the last of3d_plan_stage_times
     double stage_ms[kStages] = {};
@@ -1060,9 +1064,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const int nb = (int)(R.zb1 - R.zb0), ng = (int)(R.zg1 - R.zg0), no = (int)(R.zo1 - R.zo0);
     hipEvent_t* evs = p->host_ev ? p->ev
                       : (p->timing_slots ? &p->tev[(size_t)(p->tcount % p->timing_slots) * (kStages + 1)] : nullptr);
+    // boundary i opens stage i and closes stage i-1; untimed stages get no events
+    // (every event is a barrier packet between kernels: a few microseconds each)
+    const unsigned bmask = p->host_ev ? ~0u : (p->timing_mask | (p->timing_mask << 1));
 #define OF3D_MARK(i) \
     do { \
-        if (evs) OF3D_HIP(hipEventRecord(evs[i], s)); \
+        if (evs && ((bmask >> (i)) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s)); \
     } while (0)
     OF3D_MARK(0);
     // K0 + K1 — frames equally spaced (one stack) are addressed by stride
@@ -1445,6 +1452,17 @@ int of3d_plan_set_timing(of3d_plan* p, int slots) {
     return 0;
 }
 
+int of3d_plan_set_timing_mask(of3d_plan* p, unsigned mask) {
+    if (!p) return fail("of3d: null plan");
+    mask &= (1u << kStages) - 1;
+    if (!mask) return fail("of3d: timing mask selects no stage");
+    OF3D_HIP(hipSetDevice(p->device));
+    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
+    p->timing_mask = mask;
+    p->tcount = 0;
+    return 0;
+}
+
 int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
     if (!p || !ms) return fail("of3d: null argument");
     if (!p->timing_slots) return fail("of3d: timing not enabled on this plan");
@@ -1454,14 +1472,17 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
     std::vector<double> acc(kStages, 0.0);
     for (int64_t j = 0; j < n; ++j) {
         hipEvent_t* e = &p->tev[(size_t)j * (kStages + 1)];
-        OF3D_HIP(hipEventSynchronize(e[kStages]));
+        int last = kStages;
+        while (!((p->timing_mask >> (last - 1)) & 1u)) --last;  // closing boundary of the last timed stage
+        OF3D_HIP(hipEventSynchronize(e[last]));
         for (int i = 0; i < kStages; ++i) {
+            if (!((p->timing_mask >> i) & 1u)) continue;
             float t = 0.f;
             OF3D_HIP(hipEventElapsedTime(&t, e[i], e[i + 1]));
             acc[i] += t;
         }
     }
-    for (int i = 0; i < m; ++i) ms[i] = acc[i] / (double)n;
+    for (int i = 0; i < m; ++i) ms[i] = ((p->timing_mask >> i) & 1u) ? acc[i] / (double)n : -1.0;
     p->tcount = 0;
     return m;
 }
