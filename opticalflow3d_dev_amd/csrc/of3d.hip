@@ -66,6 +66,8 @@ struct DevTaps {
     const F* s;  // smooth  (rs)
     const F* t;  // tderiv  (rt, antisymmetric)
     const F* w;  // window  (rw)
+    // step-order copies (hr[q] = w[q], q < r, then kTapPad zeros), see lds_pass
+    const F *gr, *dr, *sr, *tr, *wr;
     int rd, rs, rt, rw;
 };
 
@@ -90,14 +92,22 @@ __device__ __forceinline__ F ldf(const void* p, size_t i) {
 // (q+i) and (q-i); each lives in a ring of M slots (L[m % M], U[m % M]), and
 // the q loop is unrolled by M so every slot index is a compile-time constant.
 // Per step: 2 LDS reads, 3R fp64 ops, ~3R live doubles, any radius.
-template <int R, bool ANTI, int D = 1, bool WRAP = false, typename F>
-__device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int base, const F* __restrict__ h, int r,
-                                         F (&out)[R], int wmask = 0) {
+// Weights: h[0] is the centre tap; hr[q] = h[r - q] = w[q] is the weight of step
+// q (outermost tap first), padded with kTapPad zeros past hr[r - 1].  PRE: each
+// M-step block takes its M weights with one uniform load issued a block ahead
+// (no scalar load + wait inside the steps; costs 2M registers, so kernels at
+// their register cap keep PRE off).
+constexpr int kTapPad = 8;  // >= the largest M
+
+template <int R, bool ANTI, bool PRE = true, int D = 1, bool WRAP = false, typename F>
+__device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int base, const F* __restrict__ h,
+                                         const F* __restrict__ hr, int r, F (&out)[R], int wmask = 0) {
     // WRAP: the staged line is a ring of (wmask + 1) positions (power of two)
     auto at = [&](int i) { return WRAP ? s[(i & wmask) * st] : s[i * st]; };
     // Ring of M = R + D - 1 slots per stream: the two reads issued after step q
     // are first consumed at step q + D (prefetch distance D hides LDS latency).
     constexpr int M = R + D - 1;
+    static_assert(M <= kTapPad, "tap padding too short for this ring");
     F L[M], U[M];
 #pragma unroll
     for (int i = 0; i < R; ++i) out[i] = at(base + i) * h[0];
@@ -105,9 +115,14 @@ __device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int ba
     for (int m = 0; m < M; ++m) L[m] = at(base - r + m);           // S_lo[0 .. M-1]
 #pragma unroll
     for (int m = -(R - 1); m < D; ++m) U[((m % M) + M) % M] = at(base + r - m);  // S_hi[-(R-1) .. D-1]
+    F wb[M];  // weights of the current block
+    if constexpr (PRE) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) wb[m] = hr[m];
+    }
     auto step = [&](int q, auto jc) {  // phase j = q mod M (compile-time)
         constexpr int j = decltype(jc)::value;
-        const F wk = h[r - q];
+        const F wk = PRE ? wb[j] : hr[q];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const F lo = L[(j + i) % M];
@@ -119,9 +134,18 @@ __device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int ba
     };
     int q = 0;
     for (; q + M <= r; q += M) {
+        F wn[M];  // next block's weights, in flight during this block
+        if constexpr (PRE) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) wn[m] = hr[q + M + m];
+        }
         [&]<int... J>(std::integer_sequence<int, J...>) {
             (step(q + J, std::integral_constant<int, J>{}), ...);
         }(std::make_integer_sequence<int, M>{});
+        if constexpr (PRE) {
+#pragma unroll
+            for (int m = 0; m < M; ++m) wb[m] = wn[m];
+        }
     }
     const int t = r - q;  // 0 .. M-1 remaining steps
     [&]<int... J>(std::integer_sequence<int, J...>) {
@@ -277,13 +301,13 @@ __global__ __launch_bounds__(256, OF3D_K1_OCC) void k_grad_xy(const T* __restric
         {
             F a[K1_R];
             const int base = rd + w * K1_R;
-            lds_pass<K1_R, false>(sT + lane, 64, base, tp.g, rd, a);
+            lds_pass<K1_R, false, false>(sT + lane, 64, base, tp.g, tp.gr, rd, a);
 #pragma unroll
             for (int i = 0; i < K1_R; ++i) sA1[(w * K1_R + i) * 64 + lane] = a[i];
-            lds_pass<K1_R, true>(sI + lane, 64, base, tp.d, rd, a);
+            lds_pass<K1_R, true, false>(sI + lane, 64, base, tp.d, tp.dr, rd, a);
 #pragma unroll
             for (int i = 0; i < K1_R; ++i) sA2[(w * K1_R + i) * 64 + lane] = a[i];
-            lds_pass<K1_R, false>(sI + lane, 64, base, tp.s, rs, a);
+            lds_pass<K1_R, false, false>(sI + lane, 64, base, tp.s, tp.sr, rs, a);
 #pragma unroll
             for (int i = 0; i < K1_R; ++i) sA3[(w * K1_R + i) * 64 + lane] = a[i];
         }
@@ -332,6 +356,7 @@ __global__ __launch_bounds__(256) void k_grad_z(const F* __restrict__ B, int zb0
     const int f = blockIdx.z & 3;
     const int zc = blockIdx.z >> 2;
     const F* h = f == 0 ? tp.g : (f == 3 ? tp.d : tp.s);
+    const F* hr = f == 0 ? tp.gr : (f == 3 ? tp.dr : tp.sr);
     const int r = (f == 0 || f == 3) ? tp.rd : tp.rs;
     const int H = K2_ZC + 2 * r;
     const int lane = threadIdx.x, g = threadIdx.y;
@@ -346,9 +371,9 @@ __global__ __launch_bounds__(256) void k_grad_z(const F* __restrict__ B, int zb0
     __syncthreads();
     F out[K2_R];
     if (f == 3)
-        lds_pass<K2_R, true>(sm + lane, 64, r + g * K2_R, h, r, out);
+        lds_pass<K2_R, true>(sm + lane, 64, r + g * K2_R, h, hr, r, out);
     else
-        lds_pass<K2_R, false>(sm + lane, 64, r + g * K2_R, h, r, out);
+        lds_pass<K2_R, false>(sm + lane, 64, r + g * K2_R, h, hr, r, out);
     if (x >= nx) return;
     F* dst = G + f * fs + (size_t)y * nx + x;
 #pragma unroll
@@ -379,7 +404,8 @@ constexpr int K3_STEP = K3_YC;
 
 template <typename F, int NP, int TJ>  // TJ >= ceil(2rw / 4): window rows each thread carries over
 __global__ __launch_bounds__(256) void k_prod_wy(const F* __restrict__ G, F* __restrict__ P, int ny, int nx,
-                                                 size_t fs, const F* __restrict__ hw, int rw) {
+                                                 size_t fs, const F* __restrict__ hw, const F* __restrict__ hwr,
+                                                 int rw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* sm = reinterpret_cast<F*>(smem_raw);
     constexpr int NJ = K3_STEP / 4;  // new rows per thread per step
@@ -418,7 +444,7 @@ __global__ __launch_bounds__(256) void k_prod_wy(const F* __restrict__ G, F* __r
         const bool more = y0 + K3_STEP < ny;
         if (more) fetch(y0 + K3_STEP + h2);
         F out[K3_R];
-        lds_pass<K3_R, false>(col, 64, rw + g * K3_R, hw, rw, out);
+        lds_pass<K3_R, false, (TJ <= 8)>(col, 64, rw + g * K3_R, hw, hwr, rw, out);
         if (x < nx) {
 #pragma unroll
             for (int i = 0; i < K3_R; ++i) {
@@ -458,7 +484,8 @@ constexpr int k4_halo(int rw) { return (rw + 15) & ~15; }
 
 template <typename F, int NF, int TJ>  // TJ >= ceil(2ha / 32): tail column groups per loader lane
 __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict__ P, F* __restrict__ Q, int ny,
-                                                             int nx, size_t fs, const F* __restrict__ hw, int rw) {
+                                                             int nx, size_t fs, const F* __restrict__ hw,
+                                                             const F* __restrict__ hwr, int rw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* sm = reinterpret_cast<F*>(smem_raw);
     const int ha = k4_halo(rw);
@@ -495,7 +522,7 @@ __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict
         const bool more = x0 + K4_TX < nx;
         if (more) fetch(x0 + K4_TX + h2);
         F out[K4_R];
-        lds_pass<K4_R, false>(sm + lane * PP, 1, ha + g * K4_R, hw, rw, out);
+        lds_pass<K4_R, false, (TJ > 1)>(sm + lane * PP, 1, ha + g * K4_R, hw, hwr, rw, out);
 #pragma unroll
         for (int i = 0; i < K4_R; ++i) so[lane * OP + g * K4_R + i] = out[i];
         if (more) {
@@ -614,9 +641,9 @@ __device__ __forceinline__ void k5_solve_store(const F (&acc)[9][K5_R], int z0l,
 
 template <typename F, typename RelT, int NJ, int K5_R, int K5_G>
 __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
-                                                  size_t fs, const F* __restrict__ hw, int rw, int zo0, int nzo,
-                                                  F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
-                                                  RelT* __restrict__ rel) {
+                                                  size_t fs, const F* __restrict__ hw, const F* __restrict__ hwr,
+                                                  int rw, int zo0, int nzo, F* __restrict__ vx, F* __restrict__ vy,
+                                                  F* __restrict__ vz, RelT* __restrict__ rel) {
     constexpr int K5_ZC = K5_G * K5_R;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* sm = reinterpret_cast<F*>(smem_raw);
@@ -648,7 +675,7 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const F* __restrict__ Q,
         }
         __syncthreads();
         if (f + 1 < 9) fetch(f + 1);
-        lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
+        lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, hwr, rw, acc[f]);
     }
     if (x >= nx) return;
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
@@ -675,7 +702,8 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 // spilled registers and measured slower.)
 template <typename F, typename RelT, int NJ2, int K5_R, int K5_G, int NB>
 __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
-                                                      size_t fs, const F* __restrict__ hw, int rw, int zo0, int nzo,
+                                                      size_t fs, const F* __restrict__ hw,
+                                                      const F* __restrict__ hwr, int rw, int zo0, int nzo,
                                                       F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
                                                       RelT* __restrict__ rel) {
     constexpr int K5_ZC = K5_G * K5_R;
@@ -721,7 +749,7 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
-        lds_pass<K5_R, false>(sm + (f % NB) * HG * RPW * 64 + lane, 64, rw + g * K5_R, hw, rw, acc[f]);
+        lds_pass<K5_R, false>(sm + (f % NB) * HG * RPW * 64 + lane, 64, rw + g * K5_R, hw, hwr, rw, acc[f]);
     }
     if (x >= nx) return;
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
@@ -833,6 +861,10 @@ int build_taps(const of3d_taps* t, of3d_plan* p) {
             return fail(std::string("of3d: taps '") + e.name + "' do not have the expected (anti)symmetry");
         for (int k = 0; k <= e.r; ++k) p->htaps.push_back(e.w[e.r - k]);
     }
+    for (auto& e : f) {  // step-order copies for lds_pass: w[0 .. r-1], then kTapPad zeros
+        for (int q = 0; q < e.r; ++q) p->htaps.push_back(e.w[q]);
+        for (int z = 0; z < kTapPad; ++z) p->htaps.push_back(0.0);
+    }
     p->rd = t->rd;
     p->rs = t->rs;
     p->rt = t->rt;
@@ -853,6 +885,11 @@ DevTaps<F> dev_taps(const of3d_plan* p) {
     d.s = d.d + p->rd + 1;
     d.t = d.s + p->rs + 1;
     d.w = d.t + p->rt + 1;
+    d.gr = d.w + p->rw + 1;
+    d.dr = d.gr + p->rd + kTapPad;
+    d.sr = d.dr + p->rd + kTapPad;
+    d.tr = d.sr + p->rs + kTapPad;
+    d.wr = d.tr + p->rt + kTapPad;
     d.rd = p->rd;
     d.rs = p->rs;
     d.rt = p->rt;
@@ -1130,7 +1167,8 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     {
         dim3 g(cdiv(nx, 64), 1, ng * nf);
         int rw_arg = p->rw;
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
+        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
+                        (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
     }
     OF3D_MARK(3);
@@ -1138,7 +1176,8 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         dim3 g(1, cdiv(ny, K4_ROWS), ng * nf);
         int rw_arg = p->rw;
         const F* Pc = P;
-        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&rw_arg};
+        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
+                        (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
     }
     OF3D_MARK(4);
@@ -1148,7 +1187,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
         const F* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                        (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
+                        (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
         if (p->k5_nb) {
             const void* k5 = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
             OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
