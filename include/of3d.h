@@ -163,6 +163,18 @@ const char* of3d_stage_name(int i);
  * (calc_flow.py:526-529 writes host arrays). */
 int of3d_copy_async(void* dst, const void* src, size_t bytes, int max_blocks, void* stream);
 
+/* Downstream statistics on resident outputs (device pointers), one pass —
+ * the reference's example_analysis_script.ipynb cells 4-6:
+ * mask = rel > thresh (thresh: e.g. the 90th percentile of rel); each of
+ * vx, vy, vz multiplied by the mask, exact zeros -> NaN, then scaled to
+ * physical units ((v*xyscale)/tscale; vz with zscale); magnitude, theta =
+ * atan2(vy, vx), phi = atan(vz / sqrt(vx^2 + vy^2)).  Inputs float64 (or
+ * float32 with v_f32), rel float32 (or float64 with rel_f64); outputs
+ * float64.  2D: vz = out_vz = phi = NULL.  Enqueued on `stream`. */
+int of3d_flow_stats(const void* vx, const void* vy, const void* vz, const void* rel, int v_f32, int rel_f64,
+                    int64_t n, double thresh, double xyscale, double zscale, double tscale, double* out_vx,
+                    double* out_vy, double* out_vz, double* magnitude, double* theta, double* phi, void* stream);
+
 /* Blocking copy of n buffers on the GPU's DMA (SDMA) engines through the HSA
  * runtime: no compute units and no HIP stream involved, so a download does
  * not contend with kernels for the memory pipeline.  Host buffers must be

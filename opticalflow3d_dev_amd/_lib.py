@@ -36,7 +36,7 @@ EXPORTED = (
     "of3d_version", "of3d_last_error", "of3d_device_count", "of3d_flow3d", "of3d_flow2d",
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
-    "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask",
+    "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
 )
 
 
@@ -113,6 +113,9 @@ def load():
         lib.of3d_plan_set_timing.restype = ctypes.c_int
         lib.of3d_plan_set_timing_mask.argtypes = [P, ctypes.c_uint]
         lib.of3d_plan_set_timing_mask.restype = ctypes.c_int
+        d = ctypes.c_double
+        lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
+        lib.of3d_flow_stats.restype = ctypes.c_int
         lib.of3d_copy_async.argtypes = [P, P, ctypes.c_size_t, ctypes.c_int, P]
         lib.of3d_copy_async.restype = ctypes.c_int
         lib.of3d_dma_copy.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),

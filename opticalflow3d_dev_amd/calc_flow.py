@@ -171,14 +171,17 @@ def _now():
 
 
 def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSig=3, tSig=1, wSig=4,
-                 precision="fp64"):
+                 precision="fp64", matlab_output=False):
     """Parse a TIFF time lapse, run the flow per output frame, write TIFFs.
 
     Mirrors calc_flow.py:362-625: same checks and messages, the same
     ``OpticalFlow3D/<imNameSave>/`` (or ``OpticalFlow2D``) output folder,
     ``<imNameSave>_parameters.csv`` and ``<imNameSave>_{vx,vy,[vz,]rel}_t%04d.tiff``
-    files, the same stdout lines.  Returns None.  precision="fp32" (an
-    extension; configs[4]) runs the float32 path and writes float32 TIFFs."""
+    files, the same stdout lines.  Returns None.  Extensions: precision="fp32"
+    (configs[4]) runs the float32 path and writes float32 TIFFs;
+    matlab_output=True writes what the reference's MATLAB twin writes
+    (M/TIFFwrite.m: LZW BigTIFF, float64; rel kept fp64 as pageeig does,
+    M/calc_flow3D.m:235-236)."""
     ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
     imDir = Path(imDir)
     if not imDir.is_dir():
@@ -255,17 +258,24 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     rt = math.ceil(3 * tSig)
     if precision not in ("fp64", "fp32"):
         raise ValueError("precision must be 'fp64' or 'fp32'")
+    if matlab_output and precision != "fp64":
+        raise ValueError("matlab_output writes float64 files: use precision='fp64'")
+    writer = tf.imwrite_matlab if matlab_output else None
     if nOut > 0 and NtChunk == 2 * rt + 1:
         _process_stream(load_frame, nOut, NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix, names,
-                        precision)
+                        precision, writer)
     else:  # window and temporal taps disagree (non-integer 6*tSig+1): one upload per window
         for hh in range(0, nOut):
             loopStart = datetime.now()
             print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
             images = np.stack([load_frame(hh + jj) for jj in range(NtChunk)])
-            out = flow(images, xyzSig, tSig, wSig) if precision == "fp64" else \
-                _flow_fp32(images, spatialDimensions, xyzSig, tSig, wSig)
-            _write_frame(prefix, names, hh + NtSlice, out)
+            if matlab_output and spatialDimensions == 3:
+                out = _flow3d(images, xyzSig, tSig, wSig, rel_fp64=True)
+            elif precision == "fp64":
+                out = flow(images, xyzSig, tSig, wSig)
+            else:
+                out = _flow_fp32(images, spatialDimensions, xyzSig, tSig, wSig)
+            _write_frame(prefix, names, hh + NtSlice, out, writer=writer)
             del out, images
             print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(datetime.now() - loopStart))
 
@@ -276,16 +286,17 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
 calc_flow = process_flow
 
 
-def _write_frame(prefix, names, frame, out, pool=None):
+def _write_frame(prefix, names, frame, out, pool=None, writer=None):
     """The reference's per-frame outputs (calc_flow.py:526-529 / :579-581);
     with a thread pool the files are written concurrently."""
     tstr = str(frame).zfill(4)
     paths = [prefix + '_' + n + '_t' + tstr + '.tiff' for n in names]
+    write = writer or (lambda path, arr: tf.imwrite(path, arr, photometric='minisblack'))
     if pool is None:
         for path, arr in zip(paths, out):
-            tf.imwrite(path, arr, photometric='minisblack')
+            write(path, arr)
     else:
-        for f in [pool.submit(tf.imwrite, path, arr, photometric='minisblack') for path, arr in zip(paths, out)]:
+        for f in [pool.submit(write, path, arr) for path, arr in zip(paths, out)]:
             f.result()
 
 
@@ -294,7 +305,8 @@ class _Shape:
         self.shape = shape
 
 
-def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names, precision="fp64"):
+def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names, precision="fp64",
+                    write_fn=None):
     """process_flow's loop on a device-resident frame ring (stream.py): one
     frame read + upload per output frame; compute, download and TIFF writing
     of consecutive frames overlap.  Files and stdout lines are the reference's
@@ -308,12 +320,13 @@ def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig
         print(_now() + ' - Processing frame ' + str(NtSlice) + '...')
         _check_args(_Shape((NtChunk,) + first.shape), ndim + 1, tSig, MSG_NDIM_3D if ndim == 3 else MSG_NDIM_2D)
     dt = first.dtype.newbyteorder('=') if first.dtype.byteorder not in ('=', '|') else first.dtype
-    fs = FlowStream(ndim, first.shape, dt, xyzSig, tSig, wSig, precision=precision)
+    fs = FlowStream(ndim, first.shape, dt, xyzSig, tSig, wSig, precision=precision,
+                    rel_fp64=write_fn is not None and ndim == 3)
 
     def finish(frame, start, start_str, pending):
         print(start_str + ' - Processing frame ' + str(frame) + '...')
         try:
-            _write_frame(prefix, names, frame, pending.result(), pool)
+            _write_frame(prefix, names, frame, pending.result(), pool, write_fn)
         finally:
             pending.release()
         print(_now() + ' - Frame ' + str(frame) + ' saved.  Duration: ' + str(datetime.now() - start))

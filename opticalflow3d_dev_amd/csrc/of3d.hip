@@ -775,6 +775,46 @@ __global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t
 }
 
 // ---------------------------------------------------------------------------
+// Downstream statistics (the reference's
+// example_analysis_script.ipynb cells 4-6) in one pass over resident outputs:
+//   mask = rel > thresh; v = v*mask, v == 0 -> NaN; vx, vy *= xyscale/tscale
+//   (as (v*xyscale)/tscale), vz likewise with zscale;
+//   magnitude = sqrt((vx*vx + vy*vy) + vz*vz); theta = atan2(vy, vx);
+//   phi = atan(vz / sqrt(vx*vx + vy*vy)).  2D: vz == nullptr, no phi.
+// ---------------------------------------------------------------------------
+template <typename VT, typename RelT>
+__global__ __launch_bounds__(256) void k_flow_stats(const VT* __restrict__ vx, const VT* __restrict__ vy,
+                                                    const VT* __restrict__ vz, const RelT* __restrict__ rel, size_t n,
+                                                    double thresh, double sxy, double sz, double st,
+                                                    double* __restrict__ ox, double* __restrict__ oy,
+                                                    double* __restrict__ oz, double* __restrict__ mag,
+                                                    double* __restrict__ theta, double* __restrict__ phi) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    const double qnan = __builtin_nan("");
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const double m = ((double)rel[i] > thresh) ? 1.0 : 0.0;  // numpy: v * bool mask
+        auto fix = [&](double v, double scale) {
+            v = v * m;
+            if (v == 0.0) v = qnan;
+            return (v * scale) / st;
+        };
+        const double x = fix((double)vx[i], sxy), y = fix((double)vy[i], sxy);
+        const double xy2 = x * x + y * y;
+        ox[i] = x;
+        oy[i] = y;
+        theta[i] = atan2(y, x);
+        if (vz) {
+            const double z = fix((double)vz[i], sz);
+            oz[i] = z;
+            mag[i] = sqrt(xy2 + z * z);
+            phi[i] = atan(z / sqrt(xy2));
+        } else {
+            mag[i] = sqrt(xy2);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
 size_t dtype_size(int dt) {
@@ -1564,6 +1604,30 @@ int of3d_dma_copy(void* const* dst, const void* const* src, const size_t* bytes,
     hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
     hsa_signal_destroy(sig);
     if (!err.empty()) return fail(err.c_str());
+    return 0;
+}
+
+int of3d_flow_stats(const void* vx, const void* vy, const void* vz, const void* rel, int v_f32, int rel_f64,
+                    int64_t n, double thresh, double xyscale, double zscale, double tscale, double* out_vx,
+                    double* out_vy, double* out_vz, double* magnitude, double* theta, double* phi, void* stream) {
+    if (n < 0) return fail("of3d: negative element count");
+    if (n == 0) return 0;
+    if (!vx || !vy || !rel || !out_vx || !out_vy || !magnitude || !theta) return fail("of3d: null argument");
+    if (vz && (!out_vz || !phi)) return fail("of3d: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 32);
+    auto launch = [&](auto vt, auto rt) {
+        using VT = decltype(vt);
+        using RT = decltype(rt);
+        hipLaunchKernelGGL((k_flow_stats<VT, RT>), dim3(blocks), dim3(256), 0, s, (const VT*)vx, (const VT*)vy,
+                           (const VT*)vz, (const RT*)rel, (size_t)n, thresh, xyscale, zscale, tscale, out_vx, out_vy,
+                           out_vz, magnitude, theta, phi);
+    };
+    if (v_f32)
+        rel_f64 ? launch(float{}, double{}) : launch(float{}, float{});
+    else
+        rel_f64 ? launch(double{}, double{}) : launch(double{}, float{});
+    OF3D_HIP(hipGetLastError());
     return 0;
 }
 

@@ -47,7 +47,7 @@ class FlowStream:
     .release() hands the buffer set back (at most `depth` frames in flight)."""
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
-                 d2h_blocks=64, precision="fp64"):
+                 d2h_blocks=64, precision="fp64", rel_fp64=False):
         import torch
 
         self.torch = torch
@@ -71,8 +71,8 @@ class FlowStream:
         if precision not in ("fp64", "fp32"):
             raise ValueError("precision must be 'fp64' (bit-exact) or 'fp32'")
         self.precision = precision
-        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device,
-                              mode=_lib.OF3D_FP32 if precision == "fp32" else 0)
+        mode = (_lib.OF3D_FP32 if precision == "fp32" else 0) | (_lib.OF3D_REL_F64 if rel_fp64 else 0)
+        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device, mode=mode)
         self.ring = torch.empty((self.nwin, self.nvox), dtype=tdt, device=self.dev)
         self.order = []  # ring slots of the resident frames, oldest first
         self.free = list(range(self.nwin))
@@ -105,7 +105,10 @@ class FlowStream:
             self.dl_thread.start()
         nout = 4 if ndim == 3 else 3
         v_t = torch.float32 if precision == "fp32" else torch.float64
-        rel_t = torch.float32 if (ndim == 3 or precision == "fp32") else torch.float64
+        if precision == "fp32":
+            rel_t = torch.float32
+        else:
+            rel_t = torch.float64 if (ndim == 2 or rel_fp64) else torch.float32
         self.depth = depth
         self.d2h_blocks = d2h_blocks
         mk = lambda pin: [torch.empty(self.nvox, dtype=v_t, device=None if pin else self.dev,

@@ -374,3 +374,128 @@ def natsorted(items):
         parts = re.split(r"(\d+)", s)
         return [(0, int(p)) if p.isdigit() else (1, p) for p in parts]
     return sorted(items, key=key)
+
+
+# ---------------------------------------------------------------------------
+# MATLAB-compatible output: the reference's MATLAB twin
+# writes every output with M/TIFFwrite.m:19-38 — libtiff (MATLAB's Tiff class)
+# in BigTIFF mode 'w8', one page per z-plane, 64-bit IEEE samples, LZW.  The
+# same library writes them here, through ctypes on the system libtiff.
+# ---------------------------------------------------------------------------
+_TIFFTAG = dict(IMAGEWIDTH=256, IMAGELENGTH=257, BITSPERSAMPLE=258, COMPRESSION=259, PHOTOMETRIC=262,
+                SAMPLESPERPIXEL=277, ROWSPERSTRIP=278, PLANARCONFIG=284, SAMPLEFORMAT=339)
+_libtiff_handle = None
+
+
+def _libtiff():
+    global _libtiff_handle
+    if _libtiff_handle is None:
+        import ctypes
+
+        for name in ("libtiff.so.6", "libtiff.so.5", "libtiff.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                break
+            except OSError:
+                continue
+        else:
+            raise ImportError("MATLAB-compatible (LZW) TIFF I/O needs the system libtiff (libtiff.so.5/6)")
+        P, U32 = ctypes.c_void_p, ctypes.c_uint32
+        lib.TIFFOpen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        lib.TIFFOpen.restype = P
+        lib.TIFFSetField.restype = ctypes.c_int  # variadic: callers pass typed arguments
+        lib.TIFFGetField.restype = ctypes.c_int
+        lib.TIFFDefaultStripSize.argtypes = [P, U32]
+        lib.TIFFDefaultStripSize.restype = U32
+        lib.TIFFWriteEncodedStrip.argtypes = [P, U32, P, ctypes.c_int64]
+        lib.TIFFWriteEncodedStrip.restype = ctypes.c_int64
+        lib.TIFFReadEncodedStrip.argtypes = [P, U32, P, ctypes.c_int64]
+        lib.TIFFReadEncodedStrip.restype = ctypes.c_int64
+        lib.TIFFNumberOfStrips.argtypes = [P]
+        lib.TIFFNumberOfStrips.restype = U32
+        lib.TIFFWriteDirectory.argtypes = [P]
+        lib.TIFFWriteDirectory.restype = ctypes.c_int
+        lib.TIFFReadDirectory.argtypes = [P]
+        lib.TIFFReadDirectory.restype = ctypes.c_int
+        lib.TIFFClose.argtypes = [P]
+        lib.TIFFClose.restype = None
+        _libtiff_handle = lib
+    return _libtiff_handle
+
+
+def imwrite_matlab(path, data):
+    """Write ``data`` ((Nz,) Ny, Nx) as M/TIFFwrite.m does: BigTIFF, one page per
+    plane, IEEE float samples of the array's width (64-bit for vx/vy/vz/rel in
+    MATLAB mode), MinIsBlack, chunky, LZW, libtiff's default strip size.
+    The encoding runs in libtiff with the GIL released (ctypes), so several
+    files can be written from threads at once."""
+    import ctypes
+
+    lib = _libtiff()
+    arr = np.asarray(data)
+    if arr.dtype.kind != "f":
+        raise ValueError("MATLAB-mode outputs are floating point")
+    arr = np.ascontiguousarray(arr, dtype=arr.dtype.newbyteorder("="))
+    if arr.ndim == 2:
+        arr = arr[None]
+    if arr.ndim != 3:
+        raise ValueError("expected a 2-D image or a (z, y, x) volume")
+    nz, ny, nx = arr.shape
+    tif = lib.TIFFOpen(os.fsencode(str(path)), b"w8")
+    if not tif:
+        raise OSError("libtiff could not create " + str(path))
+    U32, I = ctypes.c_uint32, ctypes.c_int
+    T = _TIFFTAG
+    try:
+        for z in range(nz):
+            for tag, val in ((T["IMAGELENGTH"], U32(ny)), (T["IMAGEWIDTH"], U32(nx)), (T["SAMPLESPERPIXEL"], I(1)),
+                             (T["PLANARCONFIG"], I(1)), (T["BITSPERSAMPLE"], I(8 * arr.itemsize)),
+                             (T["SAMPLEFORMAT"], I(3)), (T["PHOTOMETRIC"], I(1)), (T["COMPRESSION"], I(5))):
+                if not lib.TIFFSetField(ctypes.c_void_p(tif), U32(tag), val):
+                    raise OSError("libtiff rejected tag %d" % tag)
+            rps = int(lib.TIFFDefaultStripSize(tif, 0))
+            lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["ROWSPERSTRIP"]), U32(rps))
+            plane = arr[z]
+            row_bytes = nx * arr.itemsize
+            for s, r0 in enumerate(range(0, ny, rps)):
+                chunk = plane[r0:r0 + rps]
+                if lib.TIFFWriteEncodedStrip(tif, s, chunk.ctypes.data, chunk.shape[0] * row_bytes) < 0:
+                    raise OSError("libtiff failed writing " + str(path))
+            if not lib.TIFFWriteDirectory(tif):
+                raise OSError("libtiff failed writing " + str(path))
+    finally:
+        lib.TIFFClose(tif)
+
+
+def imread_libtiff(path):
+    """Read any single-sample TIFF libtiff can decode (e.g. the LZW BigTIFFs of
+    imwrite_matlab / MATLAB's TIFFwrite) as a (pages, y, x) or (y, x) array."""
+    import ctypes
+
+    lib = _libtiff()
+    tif = lib.TIFFOpen(os.fsencode(str(path)), b"r")
+    if not tif:
+        raise OSError("libtiff could not open " + str(path))
+    T = _TIFFTAG
+    get = lambda tag, ct: (lambda v: (lib.TIFFGetField(ctypes.c_void_p(tif), ctypes.c_uint32(tag), ctypes.byref(v)),
+                                      v.value)[1])(ct())
+    pages = []
+    try:
+        while True:
+            w, h = get(T["IMAGEWIDTH"], ctypes.c_uint32), get(T["IMAGELENGTH"], ctypes.c_uint32)
+            bits, fmt = get(T["BITSPERSAMPLE"], ctypes.c_uint16), get(T["SAMPLEFORMAT"], ctypes.c_uint16) or 1
+            dt = np.dtype({1: "u", 2: "i", 3: "f"}[fmt] + str(bits // 8))
+            out = np.empty((h, w), dt)
+            buf = out.reshape(-1).view(np.uint8)
+            pos = 0
+            for s in range(lib.TIFFNumberOfStrips(tif)):
+                n = lib.TIFFReadEncodedStrip(tif, s, buf[pos:].ctypes.data, buf.size - pos)
+                if n < 0:
+                    raise OSError("libtiff failed decoding " + str(path))
+                pos += n
+            pages.append(out)
+            if not lib.TIFFReadDirectory(tif):
+                break
+    finally:
+        lib.TIFFClose(tif)
+    return pages[0] if len(pages) == 1 else np.stack(pages)

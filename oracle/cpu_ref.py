@@ -288,3 +288,31 @@ def synthetic_stack_np(shape, seed=20260206, motion=(0.3, -0.2, -0.1)):
         noise = rng.integers(-8, 9, size=sp)
         out[t] = np.clip(1000 + 300 * s + noise, 0, 65535).astype(np.uint16)
     return out
+
+
+def analysis_reference(vx, vy, vz, rel, relPer=90, xyscale=1.0, zscale=1.0, tscale=1.0):
+    """The reference's post-processing, restated from
+    src/Python/example_analysis_script.ipynb cells 4-6 (reliability percentile
+    mask, masked velocities in physical units, magnitude, theta, phi), on host
+    arrays.  vz None for 2D (then no phi and a 2-term magnitude)."""
+    relThresh = np.percentile(rel, relPer)                      # cell 4
+    relMask = rel > relThresh
+    out = {"threshold": relThresh}
+    vx = vx * relMask                                           # cell 5
+    vx[vx == 0] = np.nan
+    vx = vx * xyscale / tscale
+    vy = vy * relMask
+    vy[vy == 0] = np.nan
+    vy = vy * xyscale / tscale
+    out["vx"], out["vy"] = vx, vy
+    if vz is not None:
+        vz = vz * relMask
+        vz[vz == 0] = np.nan
+        vz = vz * zscale / tscale
+        out["vz"] = vz
+        out["magnitude"] = np.sqrt(np.power(vx, 2) + np.power(vy, 2) + np.power(vz, 2))   # cell 6
+        out["phi"] = np.arctan(vz / np.sqrt(np.power(vx, 2) + np.power(vy, 2)))
+    else:
+        out["magnitude"] = np.sqrt(np.power(vx, 2) + np.power(vy, 2))
+    out["theta"] = np.arctan2(vy, vx)
+    return out

@@ -143,3 +143,22 @@ def test_dma_copy_roundtrip():
     with pytest.raises(RuntimeError):
         pageable = np.zeros(16, np.uint8)
         _lib.dma_copy([pageable.ctypes.data], [a.data_ptr()], [16])
+
+
+def test_matlab_output_mode(tmp_path):
+    """matlab_output=True: LZW BigTIFF float64 files (M/TIFFwrite.m), read back
+    with libtiff; vx bit-identical to the default mode, rel = the fp64 eigenvalue."""
+    import importlib
+
+    cf = importlib.import_module("opticalflow3d_dev_amd.calc_flow")  # the module (the package's calc_flow is a function)
+
+    stack = _stack((8, 4, 18, 20), 6)
+    tf.imwrite(tmp_path / "m.tif", stack, imagej=True)
+    process_flow(str(tmp_path), "m", "OneTif", 3, 1, 1, 2, matlab_output=True)
+    out = tmp_path / "OpticalFlow3D" / "m"
+    ref = cf._flow3d(stack[0:7], 1, 1, 2, rel_fp64=True)
+    raw = (out / "m_vx_t0003.tiff").read_bytes()
+    assert raw[:4] == b"II+\x00"  # BigTIFF
+    for name, r in zip(("vx", "vy", "vz", "rel"), ref):
+        got = tf.imread_libtiff(out / f"m_{name}_t0003.tiff")
+        assert got.dtype == np.float64 and bits_equal(got, r)

@@ -129,3 +129,42 @@ def test_process_flow_errors(tmp_path):
     with pytest.raises(SystemExit) as e:
         process_flow(str(tmp_path), "plain", "OneTif", 4)
     assert str(e.value.code) == "ERROR: Number of spatial dimensions must be either 2 or 3."
+
+
+@pytest.mark.parametrize("shape,dtype", [((3, 17, 29), np.float64), ((40, 33), np.float64), ((2, 300, 70), np.float32)])
+def test_matlab_lzw_writer_roundtrip(tmp_path, shape, dtype):
+    """MATLAB-mode writer (M/TIFFwrite.m layout through the system libtiff):
+    BigTIFF, LZW (tag 259 = 5), IEEE samples; pixels round-trip exactly."""
+    import struct
+
+    a = np.random.default_rng(1).standard_normal(shape).astype(dtype)
+    a.flat[0] = -0.0
+    p = tmp_path / "x.tiff"
+    tf.imwrite_matlab(p, a)
+    raw = p.read_bytes()
+    assert raw[:4] == b"II+\x00"
+    ifd = struct.unpack_from("<Q", raw, 8)[0]
+    n = struct.unpack_from("<Q", raw, ifd)[0]
+    tags = {struct.unpack_from("<H", raw, ifd + 8 + 20 * i)[0]: struct.unpack_from("<Q", raw, ifd + 8 + 20 * i + 12)[0]
+            for i in range(n)}
+    assert tags[259] == 5 and tags[339] == 3 and tags[258] == 8 * a.itemsize and tags[262] == 1
+    b = tf.imread_libtiff(p)
+    assert b.dtype == a.dtype and b.shape == a.shape
+    assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_percentile_threshold_matches_numpy(dtype):
+    """analysis.percentile_threshold (order statistics + numpy's lerp) equals
+    np.percentile bit for bit (torch CPU tensors here; CUDA on the box)."""
+    import torch
+
+    from opticalflow3d_dev_amd.analysis import percentile_threshold
+
+    rng = np.random.default_rng(7)
+    for n in (1, 2, 5, 1000, 65537):
+        a = rng.standard_normal(n).astype(dtype)
+        for p in (0, 10, 33.3333, 50, 63.7, 90, 99.9, 100):
+            r = np.percentile(a, p)
+            g = percentile_threshold(torch.from_numpy(a), p)
+            assert r.dtype == g.dtype and r.tobytes() == np.asarray(g).tobytes(), (n, p)
