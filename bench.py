@@ -177,6 +177,17 @@ def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
             "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
 
 
+def max_over_ranks(values, dev):
+    """Element-wise MAX over ranks (device tensor for RCCL, host tensor for gloo)."""
+    import torch
+    import torch.distributed as dist
+
+    where = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor(values, dtype=torch.float64, device=where)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
 def timed_region(step, plan, args, world, dev):
     """warmup -> stage profile (K steps with all five stages timed, outside the timed
     region: every HIP event is a barrier packet between kernels, so timing all stages
@@ -251,7 +262,7 @@ def run_zslab(args, world, rank, local_rank, dev):
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
     fp32 = args.config in FP32_CONFIGS or args.precision == "fp32"
-    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=local_rank, timing=max(args.steps, 1),
+    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=dev.index, timing=max(args.steps, 1),
                    mode=_lib.OF3D_FP32 if fp32 else 0)
     own = zf.allocate(torch.int16, dev)
     seed = 20260206 + (5 if fp32 else 4)
@@ -268,9 +279,8 @@ def run_zslab(args, world, rank, local_rank, dev):
                                                  world, dev)
     finite = bool(torch.isfinite(outs[0][:n_out]).all().item()) if n_out else True
     if world > 1:
-        tt = torch.tensor([elapsed, 0.0 if finite else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, finite = float(tt[0].item()), tt[1].item() == 0.0
+        elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
+        finite = bad == 0.0
     if rank == 0:
         vox = nz * ny * nx
         nb, no = zf.zi1 - zf.zi0, zf.z1 - zf.z0
@@ -323,12 +333,18 @@ def main():
 
     from opticalflow3d_dev_amd import _lib, make_taps, radii
 
+    # OF3D_BENCH_BACKEND=gloo rehearses the N>1 logic with several ranks on fewer GPUs
+    # (ranks share devices round-robin); the driver's runs use RCCL ("nccl"), one GPU per rank.
+    backend = os.environ.get("OF3D_BENCH_BACKEND", "nccl")
+    gpu = local_rank % max(torch.cuda.device_count(), 1) if backend == "gloo" else local_rank
+    os.environ["OF3D_DEVICE"] = str(gpu)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if args.config in ZSLAB_CONFIGS:
         run_zslab(args, world, rank, local_rank, dev)
         if world > 1:
@@ -349,7 +365,7 @@ def main():
     d_vz = torch.empty_like(d_vx)
     d_rel = torch.empty(vox, dtype=torch.float32, device=dev)
 
-    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=local_rank, timing=max(args.steps, 1),
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=dev.index, timing=max(args.steps, 1),
                      mode=_lib.OF3D_FP32 if fp32 else 0)
     fptrs = [d_in[i].data_ptr() for i in range(nwin)]
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -360,9 +376,7 @@ def main():
 
     elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        (elapsed,) = max_over_ranks([elapsed], dev)
 
     # sanity: finite outputs
     finite = bool(torch.isfinite(d_vx).all().item())
