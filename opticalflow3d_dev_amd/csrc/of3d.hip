@@ -675,7 +675,7 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const F* __restrict__ Q,
         }
         __syncthreads();
         if (f + 1 < 9) fetch(f + 1);
-        lds_pass<K5_R, false>(buf + lane, 64, rw + g * K5_R, hw, hwr, rw, acc[f]);
+        lds_pass<K5_R, false, false>(buf + lane, 64, rw + g * K5_R, hw, hwr, rw, acc[f]);
     }
     if (x >= nx) return;
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
