@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -151,6 +153,36 @@ __device__ __forceinline__ void lds_pass(const F* __restrict__ s, int st, int ba
     [&]<int... J>(std::integer_sequence<int, J...>) {
         ((J < t ? step(q + J, std::integral_constant<int, J>{}) : void()), ...);
     }(std::make_integer_sequence<int, M - 1>{});
+}
+
+// lds_pass with a compile-time radius RW and the half taps in registers
+// (h[k] = w[RW - k]: uniform, so SGPRs): fully unrolled, no weight loads or
+// waits inside the pass, same scipy order.  Stream rings as in lds_pass
+// (prefetch distance D); reads past the last needed element are skipped.
+template <int R, int RW, int D, bool ANTI = false, typename F>
+__device__ __forceinline__ void lds_pass_c(const F* __restrict__ s, int st, int base, const F (&h)[RW + 1],
+                                           F (&out)[R]) {
+    constexpr int M = R + D - 1;
+    F L[M], U[M];
+#pragma unroll
+    for (int i = 0; i < R; ++i) out[i] = s[(base + i) * st] * h[0];
+#pragma unroll
+    for (int m = 0; m < M; ++m) L[m] = s[(base - RW + m) * st];  // S_lo[0 .. M-1]
+#pragma unroll
+    for (int m = -(R - 1); m < D; ++m) U[((m % M) + M) % M] = s[(base + RW - m) * st];  // S_hi[-(R-1) .. D-1]
+#pragma unroll
+    for (int q = 0; q < RW; ++q) {  // k = RW - q, outermost tap first
+        const int j = q % M;
+        const F wk = h[RW - q];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const F lo = L[(j + i) % M];
+            const F hi = U[((j - i) % M + M) % M];
+            out[i] = out[i] + (ANTI ? (lo - hi) : (lo + hi)) * wk;
+        }
+        if (q + M <= RW + R - 2) L[j] = s[(base - RW + q + M) * st];  // S_lo[q+M]
+        if (q + D <= RW - 1) U[(j + D) % M] = s[(base + RW - q - D) * st];  // S_hi[q+D]
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -551,6 +583,207 @@ __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict
 }
 
 // ---------------------------------------------------------------------------
+// K34: products + W y + W x in one pass (calc_flow.py:300-313 y and x passes;
+// 2D :133-141), so the W-y result never goes to HBM.
+//
+// Block = one product of one plane, a column block of CW = blockDim.x staged
+// columns (TX outputs + RW halo columns each side, clamped at the volume
+// edge), one chunk of rows.  Thread = staged column, marching down its rows:
+//   phase A (W y, registers only): the column's products live in a register
+//     ring of NR slots (row j in slot (j - y0 + RW) mod NR); the loop is
+//     unrolled by NR so every slot index is a compile-time constant, no moves,
+//     no LDS reads.  Gradient loads run PD rows ahead (raw ring of PD).  Each
+//     step writes its W-y row value into an LDS tile row (S rows per tile).
+//   phase B (W x, every S rows): the tile's S rows x TX columns through
+//     lds_pass (RB = 4 consecutive columns per item, lane = tile row, odd pitch),
+//     results through an LDS out tile to coalesced row stores.
+// Blocks are numbered XCD-aware: the blocks of one (plane, row chunk) group
+// share blockIdx.x % 8 (one XCD's L2 under round-robin placement), so the four
+// gradient rows that 9 products x column blocks read come from one L2.
+// ---------------------------------------------------------------------------
+constexpr int k34_nr(int rw, int s) { return ((2 * rw + 2 + s - 1) / s) * s; }
+// W-y tile row r starts at r cwp + 28 (r / 4): with cwp = 1 (mod 32) every row start is
+// r mod 4 (mod 32) elements (bank-conflict-free phase B, see k_prod_wyx)
+__host__ __device__ constexpr int k34_row(int r, int cwp) { return r * cwp + 28 * (r / 4); }
+__host__ __device__ constexpr int k34_tile(int s, int cwp) { return s * cwp + 28 * (s / 4); }  // per tile buffer
+
+__device__ __forceinline__ void lds_barrier() {
+    // LDS-only barrier: global loads in flight stay in flight (__syncthreads
+    // would also drain vmcnt, i.e. the phase-A prefetch)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+#ifndef OF3D_K34_OCC
+#define OF3D_K34_OCC 3
+#endif
+
+// Raw buffer access (one SGPR descriptor per plane-field, 32-bit SGPR row offset +
+// one VGPR lane offset): no per-load 64-bit address VALU, no address VGPRs.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+template <typename F>
+__device__ __forceinline__ F buf_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    if constexpr (sizeof(F) == 8)
+        return __builtin_bit_cast(F, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+    else
+        return __builtin_bit_cast(F, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+template <typename F>
+__device__ __forceinline__ void buf_st(F v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    if constexpr (sizeof(F) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
+                                              r, voff, soff, 0);
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+}
+// N consecutive values from registers, as 16-byte stores (N * sizeof(F) a multiple of 16)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+template <typename F, int N>
+__device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    constexpr int PER = 16 / (int)sizeof(F);
+    static_assert(N % PER == 0, "whole 16-byte stores");
+#pragma unroll
+    for (int i = 0; i < N; i += PER) {
+        F w[PER];
+#pragma unroll
+        for (int e = 0; e < PER; ++e) w[e] = v[i + e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), r, voff + i * (unsigned)sizeof(F), soff,
+                                               0);
+    }
+}
+
+template <typename F, int NP, int RW, int S>
+__global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
+                                                                 int nx, size_t fs, const F* __restrict__ hw,
+                                                                 int tx, int nyc, int nbx, int nyb, int cpg,
+                                                                 int ngroups) {
+    constexpr int NR = k34_nr(RW, S);
+    // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
+    constexpr int PD = sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8);
+    constexpr int RB = 4;                 // W-x outputs per item (phase B)
+    constexpr unsigned ES = sizeof(F);
+    static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sw = reinterpret_cast<F*>(smem_raw);  // two W-y tiles [2][S][cwp] (tile n in buffer n & 1)
+    const int cw = blockDim.x, cwp = cw + 1;
+    const int t = threadIdx.x;
+    // XCD-aware block decode: group g = (plane, run of cpg row chunks), member m = (chunk in the
+    // run, product, column block): one group's blocks share an XCD and are dispatched together
+    const int mb = cpg * NP * nbx;
+    const int kb = blockIdx.x >> 3;
+    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
+    if (g >= ngroups) return;
+    int m = kb % mb;
+    const int bx = m % nbx;
+    m /= nbx;
+    const int p = m % NP, ycl = m / NP;
+    const int nyg = (nyb + cpg - 1) / cpg;
+    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
+    if (yc >= nyb) return;
+    const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
+    const int xo0 = bx * tx;
+    const int txu = min(tx, nx - xo0);  // useful outputs of this block
+    const unsigned vof = (unsigned)clampi(xo0 - RW + t, 0, nx - 1) * ES;  // staged column of this thread
+    constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // as k_prod_wy
+    constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
+    const size_t pl = (size_t)zl * ny * nx;
+    const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
+    const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
+    const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+    const unsigned rowb = (unsigned)nx * ES;
+    F h[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k) h[k] = hw[k];
+    auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
+    F ring[NR], ra[PD], rb[PD];
+#pragma unroll
+    for (int i = 0; i <= 2 * RW; ++i) {
+        const unsigned o = rowoff(i);
+        ring[i] = buf_ld<F>(ra_, vof, o) * buf_ld<F>(rb_, vof, o);
+    }
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        const unsigned o = rowoff(2 * RW + 1 + i);
+        ra[(2 * RW + 1 + i) % PD] = buf_ld<F>(ra_, vof, o);
+        rb[(2 * RW + 1 + i) % PD] = buf_ld<F>(rb_, vof, o);
+    }
+    const int nseg = (txu + RB - 1) / RB;
+    // phase B: W x over tile buffer `tile` (rows r < S), RB consecutive outputs per item
+    // stored straight from registers (rows [yb, yb + nr) only).  One barrier per tile:
+    // the other buffer is being filled by phase A meanwhile.
+    // Item -> lane, conflict-free for both LDS read forms (ds_read_b64: 32-lane groups,
+    // 64 banks; ds_read2_b64: 16-lane groups, 32 banks): lane bits b5..b0 give row
+    // (b3b2) + 4 b5 and segment (b1b0) + 4 b4, and row r starts at rowoff(r) =
+    // r cwp + off(r) with rowoff(r) = r mod 4 (mod 32 doubles), so a lane reads at
+    // (b3b2) + 4 (b1b0) + 16 b4 (mod 32): 16 distinct mod 16, 32 distinct mod 32.
+    // S = 4: rows (b3b2), segment (b1b0) + 4 b4 + 8 b5.
+    constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW;  // rows / segments per wave-item group
+    constexpr int RG = S / RPW;                          // row groups
+    const int nsgw = (nseg + SPW - 1) / SPW;
+    auto phase_b = [&](const F* tile, int yb, int nr) {
+        lds_barrier();
+        for (int i = t; i < 64 * RG * nsgw; i += cw) {
+            const int l = i & 63, wg = i >> 6;
+            const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
+            const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
+            if (sg >= nseg) continue;
+            F out[RB];
+            lds_pass_c<RB, RW, 2>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
+            if (r < nr) {
+                // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
+                const int c0 = RB * sg;
+                const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
+                if (c0 + RB <= txu) {
+                    buf_st_n<F, RB>(out, rq_, vo, 0);
+                } else {
+                    for (int e = 0; e < RB; ++e)
+                        if (c0 + e < txu) buf_st<F>(out[e], rq_, vo + e * ES, 0);
+                }
+            }
+        }
+    };
+    for (int u0 = 0; u0 < nrows; u0 += NR) {
+        bool done = false;
+        [&]<int... H>(std::integer_sequence<int, H...>) {
+            (
+                [&] {
+                    if (done) return;
+                    constexpr int h0 = H * S;
+                    F* tile = sw + (((u0 + h0) / S) & 1) * k34_tile(S, cwp);
+                    [&]<int... J>(std::integer_sequence<int, J...>) {
+                        (
+                            [&] {
+                                constexpr int j = h0 + J;  // step within the ring period
+                                constexpr int ic = j + 2 * RW + 1;
+                                ring[ic % NR] = ra[ic % PD] * rb[ic % PD];
+                                const unsigned o = rowoff(u0 + ic + PD);
+                                ra[ic % PD] = buf_ld<F>(ra_, vof, o);
+                                rb[ic % PD] = buf_ld<F>(rb_, vof, o);
+                                F acc = ring[(j + RW) % NR] * h[0];
+#ifndef OF3D_EXP_NOA
+#pragma unroll
+                                for (int k = RW; k >= 1; --k)
+                                    acc = acc + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
+#endif
+                                tile[k34_row(j % S, cwp) + t] = acc;
+#ifdef OF3D_K34_SB
+                                __builtin_amdgcn_sched_barrier(0);  // keep steps apart: bounded live ranges
+#endif
+                            }(),
+                            ...);
+                    }(std::make_integer_sequence<int, S>{});
+                    const int yb = u0 + h0;
+                    phase_b(tile, y0 + yb, min(S, nrows - yb));
+                    if (yb + S >= nrows) done = true;
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NR / S>{});
+        if (done) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Solves.  Expression trees copied from calc_flow.py:337-340 (3D) and
 // :154-168 (2D); numpy's x**-1 is a correctly rounded reciprocal, x**2 = x*x.
 // ---------------------------------------------------------------------------
@@ -863,6 +1096,12 @@ struct of3d_plan {
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
     size_t k5d_lds = 0;
+    // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
+    struct {
+        const void* fn = nullptr;
+        int cw = 0, s = 0, tx = 0, nbx = 0;
+        size_t lds = 0;
+    } k34;
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
@@ -1061,6 +1300,81 @@ const void* k4_kernel(int nf, int rw) {
     return tj <= 1 ? (const void*)k_wx<F, 5, 1> : (tj == 2 ? (const void*)k_wx<F, 5, 2> : (const void*)k_wx<F, 5, 3>);
 }
 
+// K34 instances: W radii with a compiled register ring (others use K3 + K4)
+template <typename F, int NP>
+const void* k34_fn(int rw, int s) {
+#define OF3D_K34(RW, SA, SB)                                    \
+    case RW:                                                    \
+        if (s == SA) return (const void*)k_prod_wyx<F, NP, RW, SA>; \
+        if (s == SB) return (const void*)k_prod_wyx<F, NP, RW, SB>; \
+        return nullptr;
+    switch (rw) {
+        OF3D_K34(12, 16, 8)
+        OF3D_K34(15, 16, 8)
+        OF3D_K34(21, 8, 4)  // register ring of 44-48 rows: shorter tiles
+        default: return nullptr;
+    }
+#undef OF3D_K34
+}
+
+// K34 geometry: waves per block nw in {1, 2, 4} (staged columns cw = 64 nw,
+// tx = (cw - 2rw) & ~3 outputs) and tile rows S.  Fewest staged lanes over the
+// row (halo + idle lanes) among the shapes that keep >= 8 waves per CU resident
+// (LDS and registers from the occupancy API), ties to the higher occupancy.
+template <typename F>
+int k34_setup(of3d_plan* p, int np) {
+    p->k34 = {};
+    if (const char* e = getenv("OF3D_K34"); e && e[0] == '0') return 0;
+    const int rw = p->rw, nx = (int)p->nx;
+    const size_t es = sizeof(F);
+    if ((size_t)p->ny * p->nx * es > 0x7fffffffu) return 0;  // 32-bit buffer offsets within a plane
+    long best_lanes = 0;
+    int best_waves = 0;
+    const char* env_nw = getenv("OF3D_K34_NW");  // overrides (experiments)
+    const char* env_s = getenv("OF3D_K34_S");
+    for (int s : {16, 8, 4}) {
+        if (env_s && atoi(env_s) != s) continue;
+        const void* fn = np == 9 ? k34_fn<F, 9>(rw, s) : k34_fn<F, 5>(rw, s);
+        if (!fn) continue;
+        for (int nw : {1, 2, 4, 8}) {  // launch bound 512
+            // blocks of 5-7 waves measured as if one block per CU fitted (c2: nw 5, 6, 7 all
+            // ~300 us vs 242 us at nw 2); keep whole-SIMD multiples
+            if (env_nw ? atoi(env_nw) != nw : nw == 8) continue;
+            const int cw = 64 * nw, tx = (cw - 2 * rw) & ~3;  // tx: whole phase-B items
+            if (tx < 8) continue;
+            const int nbx = (nx + tx - 1) / tx;
+            const size_t lds = (size_t)2 * k34_tile(s, cw + 1) * es;  // two W-y tiles
+            if (lds > 160 * 1024) continue;
+            OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            int nb = 0;
+            OF3D_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, cw, lds));
+            const int waves = nb * nw;
+            if (waves == 0) continue;
+            const long lanes = (long)nbx * cw;
+            const bool ok = waves >= 8, best_ok = best_waves >= 8;
+            const bool better = !p->k34.fn || (ok && !best_ok) ||
+                                (ok == best_ok && (ok ? (lanes < best_lanes || (lanes == best_lanes && waves > best_waves))
+                                                      : waves > best_waves));
+            if (better) {
+                p->k34.fn = fn;
+                p->k34.cw = cw;
+                p->k34.s = s;
+                p->k34.tx = tx;
+                p->k34.nbx = nbx;
+                p->k34.lds = lds;
+                best_lanes = lanes;
+                best_waves = waves;
+            }
+        }
+    }
+    if (p->k34.fn)
+        OF3D_HIP(hipFuncSetAttribute(p->k34.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (getenv("OF3D_VERBOSE") && p->k34.fn)
+        fprintf(stderr, "of3d: K34 cw=%d s=%d tx=%d nbx=%d lds=%zu lanes=%ld waves/CU=%d\n", p->k34.cw, p->k34.s,
+                p->k34.tx, p->k34.nbx, p->k34.lds, best_lanes, best_waves);
+    return 0;
+}
+
 template <typename F>
 int set_attrs_t(of3d_plan* p) {
     const size_t e = sizeof(F);
@@ -1088,7 +1402,8 @@ int set_attrs_t(of3d_plan* p) {
         rc |= attr(k5_dma_kernel<F, float>(p->rw, p->k5_nb), p->k5d_lds) |
               attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
     }
-    return rc ? -1 : 0;
+    if (rc) return -1;
+    return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
 }
 
 int set_attrs(of3d_plan* p) {
@@ -1202,8 +1517,32 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     }
     OF3D_MARK(2);
     F* P = p->ndim == 3 ? X : Y;
-    F* Q = p->ndim == 3 ? Y : X;
+    F* Q = p->ndim == 3 ? Y : X;  // W-xy result (K4), or P when K34 writes it (G lives in Q's buffer)
+    if (p->k34.fn) Q = P;
     const int nf = p->ndim == 3 ? 9 : 5;
+    if (p->k34.fn) {
+        // fused products + W y + W x (stage "prod_wy"; stage "wx" stays empty)
+        const auto& k = p->k34;
+        const int nyb_max = std::max(1, ny / 32);  // row chunks of >= 32 rows
+        // enough blocks for ~4 rounds of 2 resident blocks on each of 256 CUs
+        int nyb = 1;
+        while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < 4L * 256 * 2) ++nyb;
+        int nyc = (ny + nyb - 1) / nyb;
+        nyc = (nyc + k.s - 1) / k.s * k.s;
+        nyb = (ny + nyc - 1) / nyc;
+        // groups share an XCD: all row chunks of a plane when there are planes enough to
+        // spread over the 8 XCDs (their halo rows then come from one L2), else one chunk each
+        int cpg = ng >= 32 ? nyb : 1;
+        int groups = ng * ((nyb + cpg - 1) / cpg);
+        const int mb = cpg * nf * k.nbx;
+        const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
+        int tx = k.tx, nbx = k.nbx;
+        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+                        (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
+        static const size_t ldsx = getenv("OF3D_K34_LDSX") ? (size_t)atol(getenv("OF3D_K34_LDSX")) : 0;  // experiments
+        OF3D_HIP(hipLaunchKernel(k.fn, dim3(blocks), dim3(k.cw), args, k.lds + ldsx, s));
+        OF3D_MARK(3);
+    } else {
     {
         dim3 g(cdiv(nx, 64), 1, ng * nf);
         int rw_arg = p->rw;
@@ -1219,6 +1558,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
                         (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
+    }
     }
     OF3D_MARK(4);
     if (p->ndim == 3) {

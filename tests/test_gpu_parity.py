@@ -65,6 +65,12 @@ SEEDED_3D = [
     ((7, 6, 30, 40), (1, 1, 2), np.float64),
     ((7, 6, 30, 40), (1, 1, 2), np.int64),      # host cast to float64, as the reference does
     ((7, 6, 30, 40), (1, 1, 2), ">u2"),         # big-endian (TIFF 'MM') input
+    # fused products + W y + W x (K34) geometry: several column blocks, row chunks
+    # not a multiple of the tile, columns shorter than the register ring, rw 12/15/21
+    ((7, 4, 37, 600), (1, 1, 5), np.uint16),
+    ((7, 3, 300, 50), (1, 1, 4), np.uint16),
+    ((7, 3, 5, 20), (1, 1, 7), np.uint16),
+    ((7, 2, 70, 1100), (1, 1, 7), np.uint16),
 ]
 
 
@@ -96,6 +102,8 @@ SEEDED_2D = [
     ((9, 64, 200), (1.5, 1.3, 3.7), np.float32),
     ((7, 1, 50), (1, 1, 2), np.uint16),
     ((7, 50, 1), (1, 1, 2), np.uint16),
+    ((7, 333, 531), (1, 1, 7), np.uint16),
+    ((7, 3, 900), (1, 1, 5), np.uint16),
 ]
 
 
