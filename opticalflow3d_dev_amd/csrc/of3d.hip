@@ -988,6 +988,80 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
+// K5c: the LDS-DMA W z + solve with a compile-time window radius (taps in SGPRs,
+// lds_pass_c: no weight loads or waits inside the passes) and narrow blocks: CB = 32
+// columns x 2 z-groups per wave, 4 waves (256 threads), R planes per z-group, so a
+// block holds ZC = 8 R output planes of 32 columns and its window of ZC + 2RW planes
+// per field takes NB buffers of HG 1-KiB row groups (fp64, RW 15: 24 KiB each).  Two
+// blocks fit a CU: one block's prologue / epilogue overlaps another's passes.
+template <typename F, typename RelT, int RW, int NB>
+__global__ __launch_bounds__(256, 2) void k_wz_solve_c(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
+                                                    size_t fs, const F* __restrict__ hw, int zo0, int nzo,
+                                                    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
+                                                    RelT* __restrict__ rel) {
+    constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // columns per block, waves, z-groups per wave
+    constexpr int R = 8, ZC = NW * LPC * R;         // planes per z-group, output planes per block
+    constexpr int H = ZC + 2 * RW;                  // window rows (planes)
+    constexpr int EPL = 16 / (int)sizeof(F);        // elements per lane per DMA
+    constexpr int LPR = CB / EPL;                   // lanes per window row
+    constexpr int RPWI = 64 / LPR;                  // window rows per wave-instruction (1 KiB)
+    constexpr int HG = (H + RPWI - 1) / RPWI;       // row groups per window
+    constexpr int NJ2 = (HG + NW - 1) / NW;         // row groups per wave
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = lane % CB, gz = w * LPC + lane / CB;
+    const int x = blockIdx.x * CB + col;
+    const int y = blockIdx.y;
+    const int zc0 = zo0 + blockIdx.z * ZC;
+    const size_t ps = (size_t)ny * nx;
+    const int xc = min((int)blockIdx.x * CB + EPL * (lane % LPR), nx - EPL);  // this lane's DMA columns
+    const F* qrow = Q + (size_t)y * nx + xc;
+    const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
+    F h[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k) h[k] = hw[k];
+    auto issue = [&](int f, int b) {
+        const F* q = qrow + f * fs;
+        const unsigned lb = lds0 + (unsigned)(b * HG * 1024);
+#pragma unroll
+        for (int j = 0; j < NJ2; ++j) {
+            const int pg = min(w + NW * j, HG - 1);  // surplus slots repeat the last group: equal counts per wave
+            const int row = min(RPWI * pg + lane / LPR, H - 1);
+            const F* src = q + (size_t)(clampi(zc0 - RW + row, 0, nz - 1) - zq0) * ps;
+            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(pg * 1024)));
+        }
+    };
+    F acc[9][R];
+#pragma unroll
+    for (int f = 0; f < NB - 1; ++f) issue(f, f);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+        // as k_wz_solve_dma: field f landed, the buffer the next issue overwrites is free
+        const int ahead = min(NB - 2, 8 - f);
+        if (ahead >= 2)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * NJ2) : "memory");
+        else if (ahead == 1)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NJ2) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
+        lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
+        // pin the pass here: without it the compiler sinks every field's arithmetic below the
+        // last barrier and keeps all 9 windows' LDS reads live in registers (spills)
+#pragma unroll
+        for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
+    }
+    if (x >= nx) return;
+    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
+}
+constexpr int k5c_zc() { return 64; }  // output planes per K5c block
+template <typename F>
+constexpr int k5c_groups(int rw) {
+    constexpr int rpwi = 64 / (32 / (16 / (int)sizeof(F)));
+    return (k5c_zc() + 2 * rw + rpwi - 1) / rpwi;
+}
+
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
 template <typename F>
 __global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t fs, int n, F* __restrict__ vx,
@@ -1096,6 +1170,9 @@ struct of3d_plan {
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
     size_t k5d_lds = 0;
+    // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
+    const void* k5c = nullptr;
+    size_t k5c_lds = 0;
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct {
         const void* fn = nullptr;
@@ -1375,6 +1452,35 @@ int k34_setup(of3d_plan* p, int np) {
     return 0;
 }
 
+// K5c instances (window radii with a compiled pass; others use k_wz_solve_dma)
+template <typename F, typename RelT>
+const void* k5c_fn(int rw, int nb) {
+#define OF3D_K5C(RW) \
+    case RW: return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3> : (const void*)k_wz_solve_c<F, RelT, RW, 2>;
+    switch (rw) {
+        OF3D_K5C(12)
+        OF3D_K5C(15)
+        OF3D_K5C(21)
+        default: return nullptr;
+    }
+#undef OF3D_K5C
+}
+
+template <typename F>
+int k5c_setup(of3d_plan* p) {
+    p->k5c = nullptr;
+    if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
+    if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
+    const size_t buf = (size_t)k5c_groups<F>(p->rw) * 1024;
+    const int nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;  // two blocks per CU
+    const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb) : k5c_fn<F, float>(p->rw, nb);
+    if (!fn) return 0;
+    p->k5c_lds = nb * buf;
+    OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
+    p->k5c = fn;
+    return 0;
+}
+
 template <typename F>
 int set_attrs_t(of3d_plan* p) {
     const size_t e = sizeof(F);
@@ -1403,6 +1509,7 @@ int set_attrs_t(of3d_plan* p) {
               attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
     }
     if (rc) return -1;
+    if (k5c_setup<F>(p)) return -1;
     return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
 }
 
@@ -1568,7 +1675,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         const F* Qc = Q;
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-        if (p->k5_nb) {
+        if (p->k5c) {
+            dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc()));
+            void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+                             (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
+            OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, s));
+        } else if (p->k5_nb) {
             const void* k5 = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
             OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
         } else {
