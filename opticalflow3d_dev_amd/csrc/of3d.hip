@@ -684,6 +684,10 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
     const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
     const int xo0 = bx * tx;
     const int txu = min(tx, nx - xo0);  // useful outputs of this block
+    // waves with no staged column (the last column block of a row is often narrow)
+    // leave at once; barriers count only the waves still running
+    const int wa = (min(cw, txu + 2 * RW) + 63) >> 6, ca = 64 * wa;
+    if (t >= ca) return;
     const unsigned vof = (unsigned)clampi(xo0 - RW + t, 0, nx - 1) * ES;  // staged column of this thread
     constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // as k_prod_wy
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
@@ -723,7 +727,7 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
     const int nsgw = (nseg + SPW - 1) / SPW;
     auto phase_b = [&](const F* tile, int yb, int nr) {
         lds_barrier();
-        for (int i = t; i < 64 * RG * nsgw; i += cw) {
+        for (int i = t; i < 64 * RG * nsgw; i += ca) {
             const int l = i & 63, wg = i >> 6;
             const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
             const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
@@ -1174,11 +1178,12 @@ struct of3d_plan {
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
-    struct {
+    struct K34Geom {
         const void* fn = nullptr;
         int cw = 0, s = 0, tx = 0, nbx = 0;
         size_t lds = 0;
     } k34;
+    std::vector<K34Geom> k34_cand;  // geometries that keep >= 8 waves per CU (k34_tune picks)
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
@@ -1401,6 +1406,7 @@ const void* k34_fn(int rw, int s) {
 template <typename F>
 int k34_setup(of3d_plan* p, int np) {
     p->k34 = {};
+    p->k34_cand.clear();
     if (const char* e = getenv("OF3D_K34"); e && e[0] == '0') return 0;
     const int rw = p->rw, nx = (int)p->nx;
     const size_t es = sizeof(F);
@@ -1427,8 +1433,12 @@ int k34_setup(of3d_plan* p, int np) {
             OF3D_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, cw, lds));
             const int waves = nb * nw;
             if (waves == 0) continue;
-            const long lanes = (long)nbx * cw;
+            const long lanes = (long)(nbx - 1) * cw + 64 * ((nx - (nbx - 1) * tx + 2 * rw + 63) / 64);
             const bool ok = waves >= 8, best_ok = best_waves >= 8;
+            if (ok) {
+                OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                p->k34_cand.push_back({fn, cw, s, tx, nbx, lds});
+            }
             const bool better = !p->k34.fn || (ok && !best_ok) ||
                                 (ok == best_ok && (ok ? (lanes < best_lanes || (lanes == best_lanes && waves > best_waves))
                                                       : waves > best_waves));
@@ -1478,6 +1488,64 @@ int k5c_setup(of3d_plan* p) {
     p->k5c_lds = nb * buf;
     OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
     p->k5c = fn;
+    return 0;
+}
+
+// One K34 launch over ng planes of nf products.  Rows are cut into chunks of >= 32
+// rows (each chunk re-reads 2 rw halo rows) until there are blocks for ~4 rounds of
+// residency; blocks of one group share an XCD: all row chunks of a plane when there are
+// planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
+template <typename K, typename F>
+hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
+                      hipStream_t s) {
+    const int nyb_max = std::max(1, ny / 32);
+    int nyb = 1;
+    while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < 4L * 256 * 2) ++nyb;
+    int nyc = (ny + nyb - 1) / nyb;
+    nyc = (nyc + k.s - 1) / k.s * k.s;
+    nyb = (ny + nyc - 1) / nyc;
+    int cpg = ng >= 32 ? nyb : 1;
+    int groups = ng * ((nyb + cpg - 1) / cpg);
+    const int mb = cpg * nf * k.nbx;
+    const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
+    int tx = k.tx, nbx = k.nbx;
+    void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&hw,
+                    (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
+    return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.cw), args, k.lds, s);
+}
+
+// K34 autotune at plan creation: every candidate geometry of k34_setup timed on the
+// plan's own workspace (whole volume, contents irrelevant to the time), the fastest kept.
+// Measured picks differ by config (c2: 2-wave blocks; c3: 4-wave blocks, 4-row tiles).
+template <typename F>
+int k34_tune(of3d_plan* p) {
+    if (p->k34_cand.size() <= 1) return 0;
+    const int nf = p->ndim == 3 ? 9 : 5, ng = (int)std::min<int64_t>(p->nz, p->cap_planes);
+    F* G = (F*)(p->ndim == 3 ? p->Y : p->X);
+    F* P = (F*)(p->ndim == 3 ? p->X : p->Y);
+    const F* hw = dev_taps<F>(p).w;
+    hipEvent_t e0, e1;
+    OF3D_HIP(hipEventCreate(&e0));
+    OF3D_HIP(hipEventCreate(&e1));
+    float best = 1e30f;
+    size_t bi = 0;
+    for (size_t i = 0; i < p->k34_cand.size(); ++i) {
+        const auto& k = p->k34_cand[i];
+        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));  // warm
+        OF3D_HIP(hipEventRecord(e0, p->stream));
+        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+        OF3D_HIP(hipEventRecord(e1, p->stream));
+        OF3D_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        OF3D_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) best = ms, bi = i;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    p->k34 = p->k34_cand[bi];
+    if (getenv("OF3D_VERBOSE"))
+        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d (%.3f ms)\n", p->k34_cand.size(),
+                p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, best);
     return 0;
 }
 
@@ -1629,25 +1697,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const int nf = p->ndim == 3 ? 9 : 5;
     if (p->k34.fn) {
         // fused products + W y + W x (stage "prod_wy"; stage "wx" stays empty)
-        const auto& k = p->k34;
-        const int nyb_max = std::max(1, ny / 32);  // row chunks of >= 32 rows
-        // enough blocks for ~4 rounds of 2 resident blocks on each of 256 CUs
-        int nyb = 1;
-        while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < 4L * 256 * 2) ++nyb;
-        int nyc = (ny + nyb - 1) / nyb;
-        nyc = (nyc + k.s - 1) / k.s * k.s;
-        nyb = (ny + nyc - 1) / nyc;
-        // groups share an XCD: all row chunks of a plane when there are planes enough to
-        // spread over the 8 XCDs (their halo rows then come from one L2), else one chunk each
-        int cpg = ng >= 32 ? nyb : 1;
-        int groups = ng * ((nyb + cpg - 1) / cpg);
-        const int mb = cpg * nf * k.nbx;
-        const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
-        int tx = k.tx, nbx = k.nbx;
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                        (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
-        static const size_t ldsx = getenv("OF3D_K34_LDSX") ? (size_t)atol(getenv("OF3D_K34_LDSX")) : 0;  // experiments
-        OF3D_HIP(hipLaunchKernel(k.fn, dim3(blocks), dim3(k.cw), args, k.lds + ldsx, s));
+        OF3D_HIP(launch_k34(p->k34, G, P, ng, nf, ny, nx, fs, tp.w, s));
         OF3D_MARK(3);
     } else {
     {
@@ -1739,6 +1789,11 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * es));
     OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * es));
     OF3D_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
+        OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
+        OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
+        if ((p->fp32 ? k34_tune<float>(p.get()) : k34_tune<double>(p.get()))) return -1;
+    }
     for (auto& e : p->ev) OF3D_HIP(hipEventCreate(&e));
     *out = p.release();
     return 0;
