@@ -788,6 +788,154 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
 }
 
 // ---------------------------------------------------------------------------
+// K1c: K1 as a column march (the K34 scheme, calc_flow.py:279-288 y and x passes):
+// thread = staged column of one plane (RD halo columns each side), marching its rows.
+// Register rings of the centre frame I and of dt0 (NR rows, compile-time slots) give
+// the y passes A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I] with no LDS reads; each row
+// lands in three LDS tiles (double-buffered, S rows).  Every S rows the x passes
+// B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (dz)
+// run over the tile with lds_pass_c (same item -> lane map as k_prod_wyx) and store
+// from registers.  Same expression order as k_grad_xy: bit-identical.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T buf_ld_raw(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    if constexpr (sizeof(T) == 1)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, 0));
+    else if constexpr (sizeof(T) == 2)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
+    else
+        return buf_ld<T>(r, voff, soff);
+}
+
+template <typename T, typename F, int RD, int RS, int S>
+__global__ __launch_bounds__(256, 3) void k_grad_xy_c(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
+                                                      int nx, DevTaps<F> tp, F* __restrict__ B, size_t fs,
+                                                      int need_b4, int tx, int nyc, int nbx, int nyb) {
+    constexpr int NR = ((2 * RD + 2 + S - 1) / S) * S;
+    constexpr int PD = NR % 8 == 0 ? 8 : 4;
+    constexpr int RB = 4;
+    constexpr unsigned ES = sizeof(F);
+    static_assert(NR % PD == 0 && NR % S == 0 && RS <= RD, "ring sizes");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sm = reinterpret_cast<F*>(smem_raw);  // [2 buffers][3 tiles][k34_tile(S, cwp)]
+    const int cw = blockDim.x, cwp = cw + 1, tl = k34_tile(S, cwp);
+    const int t = threadIdx.x;
+    int b = blockIdx.x;
+    const int bx = b % nbx;
+    b /= nbx;
+    const int yc = b % nyb, z = b / nyb;
+    const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
+    const int xo0 = bx * tx;
+    const int txu = min(tx, nx - xo0);
+    const int wa = (min(cw, txu + 2 * RD) + 63) >> 6, ca = 64 * wa;
+    if (t >= ca) return;
+    const size_t ps = (size_t)ny * nx;
+    const unsigned gx = (unsigned)clampi(xo0 - RD + t, 0, nx - 1);
+    const auto ri_ = buf_rsrc(Ic + (size_t)z * ps);
+    const auto rt_ = buf_rsrc(D0 + (size_t)z * ps);
+    F* bz = B + (size_t)z * ps + xo0;
+    const auto rb0 = buf_rsrc(bz), rb1 = buf_rsrc(bz + fs), rb2 = buf_rsrc(bz + 2 * fs), rb3 = buf_rsrc(bz + 3 * fs);
+    F hg[RD + 1], hd[RD + 1], hs[RS + 1];
+#pragma unroll
+    for (int k = 0; k <= RD; ++k) hg[k] = tp.g[k], hd[k] = tp.d[k];
+#pragma unroll
+    for (int k = 0; k <= RS; ++k) hs[k] = tp.s[k];
+    auto row = [&](int idx) { return (unsigned)clampi(y0 - RD + idx, 0, ny - 1) * (unsigned)nx; };
+    F ri[NR], rt[NR], pt[PD];
+    T pi[PD];
+#pragma unroll
+    for (int i = 0; i <= 2 * RD; ++i) {
+        const unsigned o = row(i);
+        ri[i] = (F)buf_ld_raw<T>(ri_, gx * (unsigned)sizeof(T), o * (unsigned)sizeof(T));
+        rt[i] = buf_ld<F>(rt_, gx * ES, o * ES);
+    }
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        const unsigned o = row(2 * RD + 1 + i);
+        pi[(2 * RD + 1 + i) % PD] = buf_ld_raw<T>(ri_, gx * (unsigned)sizeof(T), o * (unsigned)sizeof(T));
+        pt[(2 * RD + 1 + i) % PD] = buf_ld<F>(rt_, gx * ES, o * ES);
+    }
+    const int nseg = (txu + RB - 1) / RB;
+    constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW, RG = S / RPW;
+    const int nsgw = (nseg + SPW - 1) / SPW;
+    const unsigned rowb = (unsigned)nx * ES;
+    auto store = [&](const F (&v)[RB], __amdgpu_buffer_rsrc_t rs, unsigned vo, int c0) {
+        if (c0 + RB <= txu) {
+            buf_st_n<F, RB>(v, rs, vo, 0);
+        } else {
+            for (int e = 0; e < RB; ++e)
+                if (c0 + e < txu) buf_st<F>(v[e], rs, vo + e * ES, 0);
+        }
+    };
+    auto phase_b = [&](const F* tiles, int yb, int nr) {
+        lds_barrier();
+        for (int i = t; i < 64 * RG * nsgw; i += ca) {
+            const int l = i & 63, wg = i >> 6;
+            const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
+            const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
+            if (sg >= nseg || r >= nr) continue;
+            const int c0 = RB * sg, base = RD + RB * sg;
+            const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
+            const int ro = k34_row(r, cwp);
+            F o[RB];
+            lds_pass_c<RB, RD, 2>(tiles + ro, 1, base, hg, o);  // dt
+            store(o, rb0, vo, c0);
+            lds_pass_c<RB, RS, 2>(tiles + tl + ro, 1, base, hs, o);  // dy
+            store(o, rb1, vo, c0);
+            lds_pass_c<RB, RD, 2, true>(tiles + 2 * tl + ro, 1, base, hd, o);  // dx
+            store(o, rb2, vo, c0);
+            if (need_b4) {
+                lds_pass_c<RB, RS, 2>(tiles + 2 * tl + ro, 1, base, hs, o);  // dz (pre-z)
+                store(o, rb3, vo, c0);
+            }
+        }
+    };
+    for (int u0 = 0; u0 < nrows; u0 += NR) {
+        bool done = false;
+        [&]<int... H>(std::integer_sequence<int, H...>) {
+            (
+                [&] {
+                    if (done) return;
+                    constexpr int h0 = H * S;
+                    F* tiles = sm + (((u0 + h0) / S) & 1) * (3 * tl);
+                    [&]<int... J>(std::integer_sequence<int, J...>) {
+                        (
+                            [&] {
+                                constexpr int j = h0 + J;
+                                constexpr int ic = j + 2 * RD + 1;
+                                ri[ic % NR] = (F)pi[ic % PD];
+                                rt[ic % NR] = pt[ic % PD];
+                                const unsigned o = row(u0 + ic + PD);
+                                pi[ic % PD] = buf_ld_raw<T>(ri_, gx * (unsigned)sizeof(T), o * (unsigned)sizeof(T));
+                                pt[ic % PD] = buf_ld<F>(rt_, gx * ES, o * ES);
+                                constexpr int c = (j + RD) % NR;
+                                F a1 = rt[c] * hg[0], a2 = ri[c] * hd[0], a3 = ri[c] * hs[0];
+#pragma unroll
+                                for (int k = RD; k >= 1; --k) {
+                                    a1 = a1 + (rt[(j + RD - k) % NR] + rt[(j + RD + k) % NR]) * hg[k];
+                                    a2 = a2 + (ri[(j + RD - k) % NR] - ri[(j + RD + k) % NR]) * hd[k];
+                                }
+#pragma unroll
+                                for (int k = RS; k >= 1; --k)
+                                    a3 = a3 + (ri[(j + RD - k) % NR] + ri[(j + RD + k) % NR]) * hs[k];
+                                const int ro = k34_row(j % S, cwp) + t;
+                                tiles[ro] = a1;
+                                tiles[tl + ro] = a2;
+                                tiles[2 * tl + ro] = a3;
+                            }(),
+                            ...);
+                    }(std::make_integer_sequence<int, S>{});
+                    const int yb = u0 + h0;
+                    phase_b(tiles, y0 + yb, min(S, nrows - yb));
+                    if (yb + S >= nrows) done = true;
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NR / S>{});
+        if (done) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Solves.  Expression trees copied from calc_flow.py:337-340 (3D) and
 // :154-168 (2D); numpy's x**-1 is a correctly rounded reciprocal, x**2 = x*x.
 // ---------------------------------------------------------------------------
@@ -1174,6 +1322,7 @@ struct of3d_plan {
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
     size_t k5d_lds = 0;
+    bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
@@ -1382,6 +1531,25 @@ const void* k4_kernel(int nf, int rw) {
     return tj <= 1 ? (const void*)k_wx<F, 5, 1> : (tj == 2 ? (const void*)k_wx<F, 5, 2> : (const void*)k_wx<F, 5, 3>);
 }
 
+// K1c instances: input dtypes u8 / u16 / f32, (rd, rs) = (3, 1), (6, 2), (9, 3) (xyzSig 1, 2, 3);
+// others use k_grad_xy.
+constexpr int K1C_S = 4;
+template <typename F>
+const void* k1c_fn(int dtype, int rd, int rs) {
+#define OF3D_K1C(T)                                                                           \
+    if (rd == 3 && rs == 1) return (const void*)k_grad_xy_c<T, F, 3, 1, K1C_S>;               \
+    if (rd == 6 && rs == 2) return (const void*)k_grad_xy_c<T, F, 6, 2, K1C_S>;               \
+    if (rd == 9 && rs == 3) return (const void*)k_grad_xy_c<T, F, 9, 3, K1C_S>;               \
+    return nullptr;
+    switch (dtype) {
+        case OF3D_U8: { OF3D_K1C(uint8_t) }
+        case OF3D_U16: { OF3D_K1C(uint16_t) }
+        case OF3D_F32: { OF3D_K1C(float) }
+        default: return nullptr;
+    }
+#undef OF3D_K1C
+}
+
 // K34 instances: W radii with a compiled register ring (others use K3 + K4)
 template <typename F, int NP>
 const void* k34_fn(int rw, int s) {
@@ -1577,6 +1745,10 @@ int set_attrs_t(of3d_plan* p) {
               attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
     }
     if (rc) return -1;
+    if (const char* e = getenv("OF3D_K1C"); e && e[0] == '0') p->k1c = false;
+    for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32})
+        if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
+            OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (k5c_setup<F>(p)) return -1;
     return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
 }
@@ -1676,7 +1848,26 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
             void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
                             (void*)&X, (void*)&fs, (void*)&need_b4};
-            OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
+            const void* k1c = p->k1c ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
+            if (k1c) {
+                // column march: 128-column blocks up to nx 512, else 256; rows in chunks of >= 32
+                const int cw = nx <= 512 ? 128 : 256;
+                int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
+                int nyc = std::min(ny, 32), nyb;
+                while (true) {
+                    nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
+                    nyb = (ny + nyc - 1) / nyc;
+                    if ((long)nb * nyb * nbx <= 8192 || nyc >= ny) break;
+                    nyc *= 2;
+                }
+                const size_t lds = (size_t)6 * k34_tile(K1C_S, cw + 1) * sizeof(F);
+                const unsigned blocks = (unsigned)((long)nb * nyb * nbx);
+                void* cargs[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&tp, (void*)&X,
+                                 (void*)&fs, (void*)&need_b4, (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb};
+                OF3D_HIP(hipLaunchKernel(k1c, dim3(blocks), dim3(cw), cargs, lds, s));
+            } else {
+                OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
+            }
         }
     }
     OF3D_MARK(1);
