@@ -2260,6 +2260,7 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
         }
     }
     for (int i = 0; i < m; ++i) ms[i] = ((p->timing_mask >> i) & 1u) ? acc[i] / (double)n : -1.0;
+    if (p->k34.fn && m > 3) ms[3] = -1.0;  // fused K34: "prod_wy" holds W x too, "wx" is empty
     p->tcount = 0;
     return m;
 }
