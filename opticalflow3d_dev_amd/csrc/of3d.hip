@@ -1146,13 +1146,13 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
 // block holds ZC = 8 R output planes of 32 columns and its window of ZC + 2RW planes
 // per field takes NB buffers of HG 1-KiB row groups (fp64, RW 15: 24 KiB each).  Two
 // blocks fit a CU: one block's prologue / epilogue overlaps another's passes.
-template <typename F, typename RelT, int RW, int NB>
-__global__ __launch_bounds__(256, 2) void k_wz_solve_c(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
+template <typename F, typename RelT, int RW, int NB, int R>
+__global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
                                                     size_t fs, const F* __restrict__ hw, int zo0, int nzo,
                                                     F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
                                                     RelT* __restrict__ rel) {
     constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // columns per block, waves, z-groups per wave
-    constexpr int R = 8, ZC = NW * LPC * R;         // planes per z-group, output planes per block
+    constexpr int ZC = NW * LPC * R;                // output planes per block (R planes per z-group)
     constexpr int H = ZC + 2 * RW;                  // window rows (planes)
     constexpr int EPL = 16 / (int)sizeof(F);        // elements per lane per DMA
     constexpr int LPR = CB / EPL;                   // lanes per window row
@@ -1207,11 +1207,11 @@ __global__ __launch_bounds__(256, 2) void k_wz_solve_c(const F* __restrict__ Q, 
     if (x >= nx) return;
     k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
-constexpr int k5c_zc() { return 64; }  // output planes per K5c block
+constexpr int k5c_zc(int r) { return 8 * r; }  // output planes per K5c block (R planes per z-group)
 template <typename F>
-constexpr int k5c_groups(int rw) {
+constexpr int k5c_groups(int rw, int r) {
     constexpr int rpwi = 64 / (32 / (16 / (int)sizeof(F)));
-    return (k5c_zc() + 2 * rw + rpwi - 1) / rpwi;
+    return (k5c_zc(r) + 2 * rw + rpwi - 1) / rpwi;
 }
 
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
@@ -1326,6 +1326,7 @@ struct of3d_plan {
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
+    int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -1632,9 +1633,11 @@ int k34_setup(of3d_plan* p, int np) {
 
 // K5c instances (window radii with a compiled pass; others use k_wz_solve_dma)
 template <typename F, typename RelT>
-const void* k5c_fn(int rw, int nb) {
+const void* k5c_fn(int rw, int nb, int r) {
 #define OF3D_K5C(RW) \
-    case RW: return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3> : (const void*)k_wz_solve_c<F, RelT, RW, 2>;
+    case RW:                                                                                            \
+        if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 4> : nullptr;            \
+        return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8> : (const void*)k_wz_solve_c<F, RelT, RW, 2, 8>;
     switch (rw) {
         OF3D_K5C(12)
         OF3D_K5C(15)
@@ -1649,10 +1652,13 @@ int k5c_setup(of3d_plan* p) {
     p->k5c = nullptr;
     if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
     if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
-    const size_t buf = (size_t)k5c_groups<F>(p->rw) * 1024;
+    const char* er = getenv("OF3D_K5C_R");
+    const int r = er ? atoi(er) : 8;
+    const size_t buf = (size_t)k5c_groups<F>(p->rw, r) * 1024;
     const int nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;  // two blocks per CU
-    const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb) : k5c_fn<F, float>(p->rw, nb);
+    const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r) : k5c_fn<F, float>(p->rw, nb, r);
     if (!fn) return 0;
+    p->k5c_r = r;
     p->k5c_lds = nb * buf;
     OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
     p->k5c = fn;
@@ -1660,15 +1666,16 @@ int k5c_setup(of3d_plan* p) {
 }
 
 // One K34 launch over ng planes of nf products.  Rows are cut into chunks of >= 32
-// rows (each chunk re-reads 2 rw halo rows) until there are blocks for ~4 rounds of
-// residency; blocks of one group share an XCD: all row chunks of a plane when there are
+// rows (each chunk re-reads 2 rw halo rows) until there are >= 4096 blocks (measured
+// 2-3 % faster than 2048 on c2/c3: shorter tail); blocks of one group share an XCD: all row chunks of a plane when there are
 // planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
 template <typename K, typename F>
 hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
                       hipStream_t s) {
     const int nyb_max = std::max(1, ny / 32);
+    static const long target = 4L * 256 * 2 * (getenv("OF3D_K34_NYBX") ? atol(getenv("OF3D_K34_NYBX")) : 2);
     int nyb = 1;
-    while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < 4L * 256 * 2) ++nyb;
+    while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
     int nyc = (ny + nyb - 1) / nyb;
     nyc = (nyc + k.s - 1) / k.s * k.s;
     nyb = (ny + nyc - 1) / nyc;
@@ -1917,7 +1924,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
         if (p->k5c) {
-            dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc()));
+            dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
             void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                              (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
             OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, s));
