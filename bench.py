@@ -152,7 +152,18 @@ def load_pmc_traffic(stage, cfg):
         with open(path) as f:
             d = json.load(f)
         ks = d.get("kernels", {})
-        vals = [e.get("hbm_bytes_per_launch") for k, e in ks.items() if k.startswith(STAGE_KERNELS[stage])]
+        # one value per kernel of the stage; of several template instances of one kernel (plan-time
+        # autotune candidates) the one dispatched most often is the one the plan uses
+        best = {}
+        for k, e in ks.items():
+            for pre in STAGE_KERNELS[stage]:
+                if k.startswith(pre):
+                    base = k.split("<")[0]
+                    rank = (e.get("dispatches", 0), -e.get("profiled_ms", 0.0))
+                    if base not in best or rank > best[base][0]:
+                        best[base] = (rank, e)
+        best = {b: e for b, (_, e) in best.items()}
+        vals = [e.get("hbm_bytes_per_launch") for e in best.values()]
         if not vals or any(v is None for v in vals):
             return None
         return round(sum(vals))

@@ -1702,6 +1702,12 @@ int k34_tune(of3d_plan* p) {
     hipEvent_t e0, e1;
     OF3D_HIP(hipEventCreate(&e0));
     OF3D_HIP(hipEventCreate(&e1));
+    // the heuristic pick (k34_setup) stays unless another shape is >= 3 % faster: stable
+    // choices from run to run (candidates within noise of each other otherwise flip)
+    size_t h0 = 0;
+    for (size_t i = 0; i < p->k34_cand.size(); ++i)
+        if (p->k34_cand[i].fn == p->k34.fn && p->k34_cand[i].cw == p->k34.cw) h0 = i;
+    std::swap(p->k34_cand[0], p->k34_cand[h0]);
     float best = 1e30f;
     size_t bi = 0;
     for (size_t i = 0; i < p->k34_cand.size(); ++i) {
@@ -1713,7 +1719,7 @@ int k34_tune(of3d_plan* p) {
         OF3D_HIP(hipEventSynchronize(e1));
         float ms = 0.f;
         OF3D_HIP(hipEventElapsedTime(&ms, e0, e1));
-        if (ms < best) best = ms, bi = i;
+        if (i == 0 ? true : ms < 0.97f * best) best = ms, bi = i;
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);

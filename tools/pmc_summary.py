@@ -55,7 +55,9 @@ def main():
     res = {}
     for k, counters in acc.items():
         d = {c: sum(v) / len(v) for c, v in counters.items()}
-        e = {"counters": d, "profiled_ms": sum(dur[k]) / len(dur[k])}
+        e = {"counters": d, "profiled_ms": sum(dur[k]) / len(dur[k]),
+             # dispatches of this kernel per profiled run (autotune candidates: 2; the kernel in use: steps)
+             "dispatches": max(len(v) for v in counters.values())}
         if "FETCH_SIZE" in d:
             e["hbm_read_bytes"] = d["FETCH_SIZE"] * 1024 * fetch_factor
         if "WRITE_SIZE" in d:
