@@ -642,7 +642,11 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 template <typename F, int N>
 __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
     constexpr int PER = 16 / (int)sizeof(F);
-    static_assert(N % PER == 0, "whole 16-byte stores");
+    if constexpr (N % PER != 0) {  // not whole 16-byte pieces: element stores
+#pragma unroll
+        for (int i = 0; i < N; ++i) buf_st<F>(v[i], r, voff + i * (unsigned)sizeof(F), soff);
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < N; i += PER) {
         F w[PER];
@@ -653,7 +657,7 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
     }
 }
 
-template <typename F, int NP, int RW, int S>
+template <typename F, int NP, int RW, int S, int RB = 4>
 __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
                                                                  int nx, size_t fs, const F* __restrict__ hw,
                                                                  int tx, int nyc, int nbx, int nyb, int cpg,
@@ -661,7 +665,7 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
     constexpr int PD = sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8);
-    constexpr int RB = 4;                 // W-x outputs per item (phase B)
+    // RB: W-x outputs per phase-B item (RB 2 measured slower: c2 +16 %, c3 +15 %; not instantiated)
     constexpr unsigned ES = sizeof(F);
     static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -755,28 +759,41 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
                     if (done) return;
                     constexpr int h0 = H * S;
                     F* tile = sw + (((u0 + h0) / S) & 1) * k34_tile(S, cwp);
+                    // two rows per step, their tap chains interleaved (ILP: a single chain issues
+                    // one fp64 op per dependent latency).  Row j+1's new product lands in row j's
+                    // outermost slot, so it is written after row j's first tap.
                     [&]<int... J>(std::integer_sequence<int, J...>) {
                         (
                             [&] {
-                                constexpr int j = h0 + J;  // step within the ring period
-                                constexpr int ic = j + 2 * RW + 1;
+                                constexpr int j = h0 + 2 * J;  // step within the ring period
+                                constexpr int ic = j + 2 * RW + 1, ic1 = ic + 1;
                                 ring[ic % NR] = ra[ic % PD] * rb[ic % PD];
                                 const unsigned o = rowoff(u0 + ic + PD);
                                 ra[ic % PD] = buf_ld<F>(ra_, vof, o);
                                 rb[ic % PD] = buf_ld<F>(rb_, vof, o);
-                                F acc = ring[(j + RW) % NR] * h[0];
+                                F p1 = ra[ic1 % PD] * rb[ic1 % PD];
+                                const unsigned o1 = rowoff(u0 + ic1 + PD);
+                                ra[ic1 % PD] = buf_ld<F>(ra_, vof, o1);
+                                rb[ic1 % PD] = buf_ld<F>(rb_, vof, o1);
+                                F a0 = ring[(j + RW) % NR] * h[0];
+                                F a1 = ring[(j + 1 + RW) % NR] * h[0];
 #ifndef OF3D_EXP_NOA
+                                a0 = a0 + (ring[j % NR] + ring[(j + 2 * RW) % NR]) * h[RW];
+                                a1 = a1 + (ring[(j + 1) % NR] + ring[(j + 1 + 2 * RW) % NR]) * h[RW];
+                                ring[ic1 % NR] = p1;  // slot of row j - RW (NR = 2 RW + 2): free now
 #pragma unroll
-                                for (int k = RW; k >= 1; --k)
-                                    acc = acc + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
+                                for (int k = RW - 1; k >= 1; --k) {
+                                    a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
+                                    a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
+                                }
+#else
+                                ring[ic1 % NR] = p1;
 #endif
-                                tile[k34_row(j % S, cwp) + t] = acc;
-#ifdef OF3D_K34_SB
-                                __builtin_amdgcn_sched_barrier(0);  // keep steps apart: bounded live ranges
-#endif
+                                tile[k34_row(j % S, cwp) + t] = a0;
+                                tile[k34_row((j + 1) % S, cwp) + t] = a1;
                             }(),
                             ...);
-                    }(std::make_integer_sequence<int, S>{});
+                    }(std::make_integer_sequence<int, S / 2>{});
                     const int yb = u0 + h0;
                     phase_b(tile, y0 + yb, min(S, nrows - yb));
                     if (yb + S >= nrows) done = true;
@@ -1553,11 +1570,11 @@ const void* k1c_fn(int dtype, int rd, int rs) {
 
 // K34 instances: W radii with a compiled register ring (others use K3 + K4)
 template <typename F, int NP>
-const void* k34_fn(int rw, int s) {
+const void* k34_fn(int rw, int s, int rb) {
 #define OF3D_K34(RW, SA, SB)                                    \
     case RW:                                                    \
-        if (s == SA) return (const void*)k_prod_wyx<F, NP, RW, SA>; \
-        if (s == SB) return (const void*)k_prod_wyx<F, NP, RW, SB>; \
+        if (s == SA) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, RW, SA>;                                     \
+        if (s == SB) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, RW, SB>;                                     \
         return nullptr;
     switch (rw) {
         OF3D_K34(12, 16, 8)
@@ -1586,7 +1603,9 @@ int k34_setup(of3d_plan* p, int np) {
     const char* env_s = getenv("OF3D_K34_S");
     for (int s : {16, 8, 4}) {
         if (env_s && atoi(env_s) != s) continue;
-        const void* fn = np == 9 ? k34_fn<F, 9>(rw, s) : k34_fn<F, 5>(rw, s);
+      for (int rb : {4, 2}) {
+        if (getenv("OF3D_K34_RB") && atoi(getenv("OF3D_K34_RB")) != rb) continue;
+        const void* fn = np == 9 ? k34_fn<F, 9>(rw, s, rb) : k34_fn<F, 5>(rw, s, rb);
         if (!fn) continue;
         for (int nw : {1, 2, 4, 8}) {  // launch bound 512
             // blocks of 5-7 waves measured as if one block per CU fitted (c2: nw 5, 6, 7 all
@@ -1622,6 +1641,7 @@ int k34_setup(of3d_plan* p, int np) {
                 best_waves = waves;
             }
         }
+      }
     }
     if (p->k34.fn)
         OF3D_HIP(hipFuncSetAttribute(p->k34.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
