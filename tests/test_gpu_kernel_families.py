@@ -1,0 +1,81 @@
+"""The column-march kernels (K1c k_grad_xy_c, K34 k_prod_wyx, K5c k_wz_solve_c) against
+the earlier kernel family (k_grad_xy, k_prod_wy + k_wx, k_wz_solve_dma / k_wz_solve) on
+the same device inputs: every output bit-identical, at sizes beyond the oracle-checked
+cases (several column blocks and row chunks, K34 autotune on).  Each family is itself
+pinned to the reference's golden vectors (test_gpu_parity.py); this covers the
+geometry paths (tail column blocks, partial tiles, XCD grouping) at scale, in fp64 and
+in the fp32 mode."""
+import os
+
+import numpy as np
+import pytest
+
+from opticalflow3d_dev_amd import _lib, make_taps, radii
+
+pytestmark = pytest.mark.gpu
+
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C")
+
+
+def _run(img, s, t, w, ndim, mode, old):
+    import torch
+
+    saved = {k: os.environ.get(k) for k in FAMILY_ENV}
+    try:
+        for k in FAMILY_ENV:
+            if old:
+                os.environ[k] = "0"
+            else:
+                os.environ.pop(k, None)
+        dev = torch.device("cuda", 0)
+        nt = img.shape[0]
+        vol = img.shape[1:] if ndim == 3 else (1,) + img.shape[1:]
+        nz, ny, nx = vol
+        rt = radii(s, t, w)[2]
+        c = nt // 2
+        win = np.ascontiguousarray(img[c - rt:c + rt + 1]).reshape((2 * rt + 1,) + vol)
+        d_in = torch.from_numpy(win.view(np.int16)).to(dev)
+        fp32 = bool(mode & _lib.OF3D_FP32)
+        vt = torch.float32 if fp32 else torch.float64
+        n = nz * ny * nx
+        outs = [torch.empty(n, dtype=vt, device=dev) for _ in range(3)]
+        rel = torch.empty(n, dtype=torch.float64 if (ndim == 2 and not fp32) else (vt if ndim == 2 else torch.float32),
+                          device=dev)
+        plan = _lib.Plan(ndim, nz, ny, nx, make_taps(s, t, w), device=0, mode=mode)
+        try:
+            plan.execute([d_in[i].data_ptr() for i in range(2 * rt + 1)], _lib.OF3D_U16, 0, 0, nz,
+                         outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), rel.data_ptr())
+            torch.cuda.synchronize(dev)
+        finally:
+            plan.close()
+        res = [o.cpu().numpy() for o in outs[:3 if ndim == 3 else 2]] + [rel.cpu().numpy()]
+        return res
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+CASES = [
+    ((13, 20, 300, 266), (2, 2, 5), 3),   # rw 15: several column blocks, tail block, partial tiles
+    ((7, 9, 130, 140), (3, 1, 4), 3),     # reference defaults: rd 9, rw 12
+    ((19, 12, 100, 530), (2, 3, 7), 3),   # rw 21 (c3 parameters)
+    ((13, 1, 700, 333), (2, 2, 5), 2),    # 2D, five products
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+@pytest.mark.parametrize("fp32", [False, True])
+def test_families_bit_identical(case, fp32):
+    shape, (s, t, w), ndim = CASES[case]
+    rng = np.random.default_rng(300 + case)
+    img = rng.integers(0, 4096, size=shape).astype(np.uint16)
+    if ndim == 2:
+        img = img[:, 0]
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    new = _run(img, s, t, w, ndim, mode, old=False)
+    ref = _run(img, s, t, w, ndim, mode, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
