@@ -1607,7 +1607,7 @@ int k34_setup(of3d_plan* p, int np) {
         if (getenv("OF3D_K34_RB") && atoi(getenv("OF3D_K34_RB")) != rb) continue;
         const void* fn = np == 9 ? k34_fn<F, 9>(rw, s, rb) : k34_fn<F, 5>(rw, s, rb);
         if (!fn) continue;
-        for (int nw : {1, 2, 4, 8}) {  // launch bound 512
+        for (int nw : {1, 2, 3, 4, 8}) {  // launch bound 512
             // blocks of 5-7 waves measured as if one block per CU fitted (c2: nw 5, 6, 7 all
             // ~300 us vs 242 us at nw 2); keep whole-SIMD multiples
             if (env_nw ? atoi(env_nw) != nw : nw == 8) continue;

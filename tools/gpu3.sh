@@ -1,4 +1,5 @@
 set -u
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernel_families.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_fam.log 2>&1; rc=$?
-tail -12 gpurun_out/pytest_fam.log; exit $rc
+export OF3D_VERBOSE=1
+CFGS="c2 c3" bash tools/ab.sh tuned: nw3:OF3D_K34_NW=3 || exit $?
+grep -h "K34 tuned" gpurun_out/ab_c*.log
