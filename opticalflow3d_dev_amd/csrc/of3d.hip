@@ -805,6 +805,82 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
 }
 
 // ---------------------------------------------------------------------------
+// K2c: the gradient z pass (calc_flow.py:279-288, axis 0) as a z march: thread = one
+// (y, x) column, lanes along x (coalesced), marching a chunk of zc output planes with a
+// register ring of NR planes per field (compile-time slots, as K34); no LDS, no
+// barriers, every input plane read once per chunk.  dt = z(G)[B1], dy = z(S)[B2],
+// dx = z(S)[B3], dz = z(D)[B4], same order as k_grad_z: bit-identical.
+// ---------------------------------------------------------------------------
+template <typename F, int RD, int RS>
+__global__ __launch_bounds__(256, 3) void k_grad_z_c(const F* __restrict__ B, int zb0, F* __restrict__ G, int zg0,
+                                                     int nzg, int nz, int plane, size_t fs, DevTaps<F> tp, int zc) {
+    constexpr int NR = ((2 * RD + 2 + 7) / 8) * 8, PD = 4;
+    static_assert(NR % PD == 0 && RS <= RD, "ring sizes");
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= plane) return;
+    const int zc0 = zg0 + blockIdx.y * zc;
+    const int nrows = min(zc, zg0 + nzg - zc0);
+    F hg[RD + 1], hd[RD + 1], hs[RS + 1];
+#pragma unroll
+    for (int k = 0; k <= RD; ++k) hg[k] = tp.g[k], hd[k] = tp.d[k];
+#pragma unroll
+    for (int k = 0; k <= RS; ++k) hs[k] = tp.s[k];
+    const F* b = B + col;
+    F* g = G + col;
+    auto src = [&](int idx) { return (size_t)(clampi(zc0 - RD + idx, 0, nz - 1) - zb0) * plane; };
+    F ring[4][NR], raw[4][PD];
+#pragma unroll
+    for (int i = 0; i <= 2 * RD; ++i) {
+        const size_t o = src(i);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) ring[f][i] = b[f * fs + o];
+    }
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        const size_t o = src(2 * RD + 1 + i);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) raw[f][(2 * RD + 1 + i) % PD] = b[f * fs + o];
+    }
+    for (int u0 = 0; u0 < nrows; u0 += NR) {
+        bool done = false;
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (
+                [&] {
+                    if (done) return;
+                    constexpr int j = J;
+                    constexpr int ic = j + 2 * RD + 1, c = (j + RD) % NR;
+                    const size_t o = src(u0 + ic + PD);
+#pragma unroll
+                    for (int f = 0; f < 4; ++f) {
+                        ring[f][ic % NR] = raw[f][ic % PD];
+                        raw[f][ic % PD] = b[f * fs + o];
+                    }
+                    F o0 = ring[0][c] * hg[0], o3 = ring[3][c] * hd[0];
+                    F o1 = ring[1][c] * hs[0], o2 = ring[2][c] * hs[0];
+#pragma unroll
+                    for (int k = RD; k >= 1; --k) {
+                        o0 = o0 + (ring[0][(j + RD - k) % NR] + ring[0][(j + RD + k) % NR]) * hg[k];
+                        o3 = o3 + (ring[3][(j + RD - k) % NR] - ring[3][(j + RD + k) % NR]) * hd[k];
+                    }
+#pragma unroll
+                    for (int k = RS; k >= 1; --k) {
+                        o1 = o1 + (ring[1][(j + RD - k) % NR] + ring[1][(j + RD + k) % NR]) * hs[k];
+                        o2 = o2 + (ring[2][(j + RD - k) % NR] + ring[2][(j + RD + k) % NR]) * hs[k];
+                    }
+                    const size_t d = (size_t)(zc0 + u0 + j - zg0) * plane;
+                    g[d] = o0;
+                    g[fs + d] = o1;
+                    g[2 * fs + d] = o2;
+                    g[3 * fs + d] = o3;
+                    if (u0 + j + 1 >= nrows) done = true;
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NR>{});
+        if (done) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K1c: K1 as a column march (the K34 scheme, calc_flow.py:279-288 y and x passes):
 // thread = staged column of one plane (RD halo columns each side), marching its rows.
 // Register rings of the centre frame I and of dt0 (NR rows, compile-time slots) give
@@ -1340,6 +1416,7 @@ struct of3d_plan {
     int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
     size_t k5d_lds = 0;
     bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
+    bool k2c = true;  // z-march K2 where instantiated (OF3D_K2C=0: k_grad_z)
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
@@ -1779,6 +1856,7 @@ int set_attrs_t(of3d_plan* p) {
     }
     if (rc) return -1;
     if (const char* e = getenv("OF3D_K1C"); e && e[0] == '0') p->k1c = false;
+    if (const char* e = getenv("OF3D_K2C"); e && e[0] == '0') p->k2c = false;
     for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32})
         if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
             OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1906,10 +1984,28 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     OF3D_MARK(1);
     const F* G;
     if (p->ndim == 3) {
-        dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
-        hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, s, X, (int)R.zb0, Y, (int)R.zg0, ng, nz, ny, nx, fs,
-                           tp);
-        OF3D_HIP(hipGetLastError());
+        const void* k2c = nullptr;
+        if (p->k2c) {
+            if (p->rd == 6 && p->rs == 2) k2c = (const void*)k_grad_z_c<F, 6, 2>;
+            if (p->rd == 3 && p->rs == 1) k2c = (const void*)k_grad_z_c<F, 3, 1>;
+        }
+        if (k2c) {
+            // z march: 256 columns per block, chunks of >= 32 planes (2 rd halo planes re-read per chunk)
+            const int plane = ny * nx;
+            int zc = std::min(ng, 32);
+            while ((long)cdiv(plane, 256) * cdiv(ng, zc) > 8192 && zc < ng) zc *= 2;
+            const F* Bc = X;
+            // input planes clamp at zb1 (= nz at the top edge): see the K5 launch
+            int zb0 = (int)R.zb0, zg0 = (int)R.zg0, ngz = ng, nzz = (int)R.zb1;
+            void* args[] = {(void*)&Bc, (void*)&zb0, (void*)&Y, (void*)&zg0, (void*)&ngz, (void*)&nzz, (void*)&plane,
+                            (void*)&fs, (void*)&tp, (void*)&zc};
+            OF3D_HIP(hipLaunchKernel(k2c, dim3(cdiv(plane, 256), cdiv(ng, zc)), dim3(256), args, 0, s));
+        } else {
+            dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
+            hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, s, X, (int)R.zb0, Y, (int)R.zg0, ng,
+                               (int)R.zb1, ny, nx, fs, tp);
+            OF3D_HIP(hipGetLastError());
+        }
         G = Y;
     } else {
         G = X;
@@ -1946,12 +2042,15 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         const K5Geom kg = k5_geom(p->rw);
         dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
         int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
+        // window planes clamp at zg1 (= nz at the volume's top edge): the rows a block
+        // loads past its last output plane stay inside the workspace's W-xy planes
+        int zq1 = (int)R.zg1;
         const F* Qc = Q;
-        void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+        void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                         (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
         if (p->k5c) {
             dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
-            void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&nz, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+            void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                              (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
             OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, s));
         } else if (p->k5_nb) {
