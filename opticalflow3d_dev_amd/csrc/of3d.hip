@@ -33,6 +33,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -257,6 +258,46 @@ __global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size
 #pragma unroll
             for (int i = 0; i < V; ++i) dt[i] = dt[i] + (a[i] - b[i]) * w;
         }
+        if constexpr (sizeof(F) == 8) {
+            double2* d = reinterpret_cast<double2*>(D0 + gi * V);
+#pragma unroll
+            for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) D0[gi * V + i] = dt[i];
+        }
+    }
+}
+
+// K0 with a compile-time temporal radius: all 2RT+1 frame loads of a lane issued
+// before the first use (the runtime-rt loop above keeps only two in flight per lane:
+// latency-bound at 4.3 TB/s on c2).  Same arithmetic order.
+template <typename T, typename F, int RT>
+__global__ __launch_bounds__(256) void k_tderiv_vec_c(Frames fr, size_t off0, size_t ngroups, const F* __restrict__ ht,
+                                                      F* __restrict__ D0) {
+    constexpr int V = K0Vec<T>::V, NW = 2 * RT + 1;
+    using Raw = typename std::conditional<K0Vec<T>::B == 8, unsigned long long, uint4>::type;
+    F h[RT + 1];
+#pragma unroll
+    for (int k = 0; k <= RT; ++k) h[k] = ht[k];
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
+        const size_t o = off0 + gi * V;
+        Raw raw[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) raw[i] = *reinterpret_cast<const Raw*>(reinterpret_cast<const T*>(fr.p[i]) + o);
+        auto val = [&](int i, int e) {
+            T t[V];
+            __builtin_memcpy(t, &raw[i], sizeof(Raw));
+            return (F)t[e];
+        };
+        F dt[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) dt[e] = val(RT, e) * h[0];
+#pragma unroll
+        for (int k = RT; k >= 1; --k)
+#pragma unroll
+            for (int e = 0; e < V; ++e) dt[e] = dt[e] + (val(RT - k, e) - val(RT + k, e)) * h[k];
         if constexpr (sizeof(F) == 8) {
             double2* d = reinterpret_cast<double2*>(D0 + gi * V);
 #pragma unroll
@@ -1538,6 +1579,24 @@ const void* k0v_kernel_dt(int dtype) {
     }
 }
 
+// compile-time-rt K0 instances: u8 / u16 / f32 input, rt 3, 6, 9 (tSig 1, 2, 3)
+template <typename F>
+const void* k0c_fn(int dtype, int rt) {
+    if (const char* e = getenv("OF3D_K0C"); e && e[0] == '0') return nullptr;
+#define OF3D_K0C(T)                                                   \
+    if (rt == 3) return (const void*)k_tderiv_vec_c<T, F, 3>;        \
+    if (rt == 6) return (const void*)k_tderiv_vec_c<T, F, 6>;        \
+    if (rt == 9) return (const void*)k_tderiv_vec_c<T, F, 9>;        \
+    return nullptr;
+    switch (dtype) {
+        case OF3D_U8: { OF3D_K0C(uint8_t) }
+        case OF3D_U16: { OF3D_K0C(uint16_t) }
+        case OF3D_F32: { OF3D_K0C(float) }
+        default: return nullptr;
+    }
+#undef OF3D_K0C
+}
+
 int k0_vec_width(int dtype) {
     const size_t es = dtype_size(dtype);
     return es == 1 ? 8 : (es == 8 ? 2 : 4);
@@ -1945,7 +2004,13 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             size_t ng = n / V;
             const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
             void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
+            const void* k0 = k0c_fn<F>(dtype, p->rt);
+            if (k0) {
+                void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
+                OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, s));
+            } else {
+                OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
+            }
         } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
             void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
@@ -1961,10 +2026,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&X, (void*)&fs, (void*)&need_b4};
             const void* k1c = p->k1c ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
             if (k1c) {
-                // column march: 128-column blocks up to nx 512, else 256; rows in chunks of >= 32
-                const int cw = nx <= 512 ? 128 : 256;
+                // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
+                static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
+                static const int nyc_env = getenv("OF3D_K1C_NYC") ? atoi(getenv("OF3D_K1C_NYC")) : 32;
+                const int cw = cw_env ? cw_env : (nx <= 256 ? 128 : 256);  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
                 int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
-                int nyc = std::min(ny, 32), nyb;
+                int nyc = std::min(ny, nyc_env), nyb;
                 while (true) {
                     nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
                     nyb = (ny + nyc - 1) / nyc;
