@@ -1110,17 +1110,20 @@ __device__ __forceinline__ double cos_small(double x) {
 __device__ __forceinline__ double eigmin3(double a, double b, double c, double d, double e, double f) {
     const double p1 = d * d + e * e + f * f;
     if (p1 == 0.0) return fmin(a, fmin(b, c));
-    const double q = (a + b + c) / 3.0;
+    // constant divisions as multiplications by the rounded reciprocal (not bit-matched
+    // anyway; an IEEE division is a ~10-instruction sequence)
+    constexpr double third = 1.0 / 3.0, sixth = 1.0 / 6.0;
+    const double q = (a + b + c) * third;
     const double aq = a - q, bq = b - q, cq = c - q;
     const double p2 = aq * aq + bq * bq + cq * cq + 2.0 * p1;
-    const double p = sqrt(p2 / 6.0);
+    const double p = sqrt(p2 * sixth);
     const double ip = 1.0 / p;
     const double B11 = aq * ip, B22 = bq * ip, B33 = cq * ip, B12 = d * ip, B13 = e * ip, B23 = f * ip;
     const double detB =
         B11 * (B22 * B33 - B23 * B23) - B12 * (B12 * B33 - B23 * B13) + B13 * (B12 * B23 - B22 * B13);
     double r = 0.5 * detB;
     r = fmin(1.0, fmax(-1.0, r));
-    const double phi = acos(r) / 3.0;
+    const double phi = acos(r) * third;
     return q - 2.0 * p * cos_small(1.0471975511965976 - phi);  // pi/3 - phi
 }
 
@@ -1962,7 +1965,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     if (R.zb1 - R.zb0 > p->cap_planes) return fail("of3d: output range exceeds the plan's workspace");
     if (frame_z0 > R.zb0) return fail("of3d: frames do not hold the stencil halo planes");
     if (dtype_size(dtype) == 0) return fail("of3d: unsupported dtype");
-    const int ny = (int)p->ny, nx = (int)p->nx, nz = (int)p->nz;
+    const int ny = (int)p->ny, nx = (int)p->nx;
     Frames fr{};
     for (int i = 0; i < 2 * p->rt + 1; ++i) {
         if (!d_frames[i]) return fail("of3d: null frame pointer");
