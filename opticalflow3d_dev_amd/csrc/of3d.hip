@@ -705,7 +705,12 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
                                                                  int ngroups) {
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
-    constexpr int PD = sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8);
+    constexpr int PD0 = sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8);
+#ifdef OF3D_K34_PD
+    constexpr int PD = NR % OF3D_K34_PD == 0 ? OF3D_K34_PD : PD0;  // experiments
+#else
+    constexpr int PD = PD0;
+#endif
     // RB: W-x outputs per phase-B item (RB 2 measured slower: c2 +16 %, c3 +15 %; not instantiated)
     constexpr unsigned ES = sizeof(F);
     static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
