@@ -6,13 +6,18 @@
 // volumes plus a per-voxel LAPACK cgeev; here the same arithmetic is a
 // five-kernel device pipeline over HBM-resident fields:
 //
-//   K1 grad_xy  : temporal derivative of the centre frame (T2) + y and x passes
-//                 of the four gradient filters (T4), LDS-tiled, clamped halos
-//   K2 grad_z   : z pass of the four gradients (T4), register-blocked along z
-//   K3 prod_wy  : the 9 (2D: 5) structure-tensor products + W y pass (T5)
-//   K4 wx       : W x pass (T5), LDS row tiles
-//   K5 wz_solve : W z pass (T5) + closed-form 3x3 solve (T6) + fp64 smallest
-//                 eigenvalue (T7);  2D: closed-form 2x2 solve + rel (T8)
+//   K0c tderiv   : temporal derivative of the centre frame (T2)
+//   K1c grad_xy  : y and x passes of the four gradient filters (T4), column march:
+//                  register rings down each column, LDS tiles for the x pass
+//   K2c grad_z   : z pass of the four gradients (T4), z march with register rings
+//   K34 prod_wyx : the 9 (2D: 5) structure-tensor products + W y (register ring)
+//                  + W x (LDS tiles) in one pass (T5); the plan autotunes its shape
+//   K5c wz_solve : W z pass (T5, LDS-DMA windows) + closed-form 3x3 solve (T6) +
+//                  fp64 smallest eigenvalue (T7);  2D: 2x2 solve + rel (T8)
+//
+// The earlier kernels (k_tderiv_vec, k_grad_xy, k_grad_z, k_prod_wy + k_wx,
+// k_wz_solve_dma / k_wz_solve) remain for radii and input types without a
+// compiled column-march instance, and as the A/B reference (bit-identical).
 //
 // Bit-exactness: every 1-D pass evaluates scipy's NI_Correlate1D order for
 // (anti)symmetric taps  o = c0*w0; for k=r..1: o += (c[-k] +- c[+k]) * w[-k]
