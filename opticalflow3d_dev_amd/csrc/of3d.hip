@@ -2037,7 +2037,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
             void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
                             (void*)&X, (void*)&fs, (void*)&need_b4};
-            const void* k1c = p->k1c ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
+            // (32-bit buffer offsets within a plane: planes up to 2 GiB)
+            const bool k1c_ok = p->k1c && (size_t)ny * nx * sizeof(F) <= 0x7fffffffu;
+            const void* k1c = k1c_ok ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
             if (k1c) {
                 // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
                 static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
