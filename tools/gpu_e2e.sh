@@ -1,3 +1,4 @@
+# End-to-end streaming benchmarks (tools/bench_e2e.py) for c2 and c3; logs under gpurun_out/.
 set -u
 cd $GRAFT_REPO_ROOT; OUT=gpurun_out; mkdir -p $OUT
 for c in c2 c3; do
