@@ -8,8 +8,9 @@ frames are resident in HBM when the timed region starts; the step runs the
 five-kernel pipeline through the C-ABI (of3d_plan_execute) and leaves
 vx, vy, vz (fp64) and rel (fp32) in HBM.
 
-Default workload = BASELINE.json configs[1] (c2): 3D 256x256x64, 13 frames,
-xyzSig=2 tSig=2 wSig=5, fp64.  --config c3 selects configs[2].
+Default workload = BASELINE.json configs[2] (c3), the largest single-GPU
+config: 3D 512x512x128, 19 frames, xyzSig=2 tSig=3 wSig=7, fp64.  --config c2
+selects configs[1]; c4/c5 are the z-slab (strong-scaling) configs.
 N > 1 (torch.distributed.run, one rank per GPU): frame replicas — every rank
 computes its own output frame (calc_flow.py:512 marks output frames as the
 independent axis); no data-path collective; value = all ranks' voxels / max
@@ -177,8 +178,25 @@ def cpu_sample_planes(nz, ny, nx, budget_s):
     return nz if est <= budget_s else max(1, int(nz * budget_s / est))
 
 
-def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
-    """Time the oracle (scipy correlate1d + LAPACK cgeev, the reference's primitives) on 1 thread."""
+def load_cpu_calibration(cfg):
+    """t_reference / t_oracle on the same input, one thread, measured in the build container
+    (tools/calibrate_cpu.py -> profiles/cpu_calibration.json; the reference itself does not
+    travel to the GPU box)."""
+    path = os.path.join(REPO, "profiles", "cpu_calibration.json")
+    try:
+        with open(path) as f:
+            cases = json.load(f)["cases"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, c in cases.items():
+        if name.split("_")[0] == cfg:
+            return dict(c, case=name)
+    return None
+
+
+def cpu_baseline(frames, s, t, w, budget_s, nz_total=None, cfg=None):
+    """Time the oracle (scipy correlate1d + LAPACK cgeev, the reference's primitives) on 1 thread;
+    reference_equiv = that rate / the committed reference-vs-oracle time ratio."""
     from threadpoolctl import threadpool_limits
 
     from oracle import cpu_ref
@@ -196,7 +214,19 @@ def cpu_baseline(frames, s, t, w, budget_s, nz_total=None):
     return {"value": round(vox / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
             "sample": f"{what} ({sub_nz}x{ny}x{nx} voxels, {nt} frames): oracle/cpu_ref.py calc_flow3D with "
                       f"scipy.ndimage.correlate1d + numpy.linalg.eigvals(complex64), 1 thread, {dt:.2f} s",
-            "seconds": round(dt, 3), "host_cpus": os.cpu_count()}
+            "seconds": round(dt, 3), "host_cpus": os.cpu_count(),
+            **calibrated(vox / dt / 1e6, cfg)}
+
+
+def calibrated(oracle_mvox_s, cfg):
+    cal = load_cpu_calibration(cfg) if cfg else None
+    if not cal:
+        return {}
+    return {"reference_equiv_value": round(oracle_mvox_s / cal["ratio"], 4),
+            "calibration": {"case": cal["case"], "t_reference_over_t_oracle": cal["ratio"],
+                            "reference_s": cal["reference_s"], "oracle_s": cal["oracle_s"],
+                            "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py, build container, "
+                                      "1 thread, same input)"}}
 
 
 def max_over_ranks(values, dev):
@@ -249,24 +279,43 @@ def timed_region(step, plan, args, world, dev):
     return elapsed, profile, dom, dom_ms
 
 
-def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, nwin, sv=8):
-    """roofline object of the bench line: the dominant stage, its HIP-event average over the
-    timed region, against HBM peak, with its PMC traffic; plus the per-stage profile and the
-    whole-frame figure."""
-    ach = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
+def frame_ops_per_voxel(rd, rs, rt, rw):
+    """SURVEY §8(d) algorithmic fp64 add/mul count per output voxel (gather form, no FMA):
+    C(rt) + 3 C(rd) + 3 [C(rd) + 2 C(rs)] + 9 + 27 C(rw) + 65 + 50 (solve + eigenvalue)."""
+    C = lambda r: 1 + 3 * r
+    return C(rt) + 3 * C(rd) + 3 * (C(rd) + 2 * C(rs)) + 9 + 27 * C(rw) + 65 + 50
+
+
+def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=8):
+    """roofline object of the bench line.
+
+    The exact fp64 path is VALU-bound by construction (28-37 algorithmic
+    flop/B against a ridge of ~4.9 flop/B; no FMA allowed by the bit-exact contract), so
+    the binding roof is the fp64 (fp32 in OF3D_FP32) add/mul issue rate: achieved = the
+    dominant kernel's algorithmic ops per launch (its §8(d) share, stage_model) / its
+    HIP-event average over the timed region, against the no-FMA VALU peak.  Beside it:
+    the HBM fraction by §8(d)'s algorithmic bytes for the whole frame (nt*2 + 3*sv + 4
+    B/voxel) over the frame's device time, the dominant kernel's PMC traffic, and the
+    per-stage profile."""
+    peak_v = FP64_VALU_PEAK_TOPS if sv == 8 else FP32_VALU_PEAK_TOPS
+    ach = model[dom]["ops"] / (dom_ms * 1e-3) / 1e12
     frame_ms = sum(profile.values())
+    k_gbs = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
+    f_gbs = frame_bytes / (frame_ms * 1e-3) / 1e9
+    f_tops = frame_ops / (frame_ms * 1e-3) / 1e12
     return {
-        "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(dom, cfg),
-        "algorithmic_bytes_per_launch": model[dom]["bytes"], "avg_launch_ms": round(dom_ms, 5),
-        "valu_tops": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12, 3),
-        "valu_frac": round(model[dom]["ops"] / (dom_ms * 1e-3) / 1e12 /
-                           (FP64_VALU_PEAK_TOPS if sv == 8 else FP32_VALU_PEAK_TOPS), 4),
+        "bound": "valu", "kernel": dom, "achieved": round(ach, 3), "peak": peak_v,
+        "unit": "Top/s (%s add/mul lane-ops, no FMA)" % ("fp64" if sv == 8 else "fp32"),
+        "frac": round(ach / peak_v, 4), "traffic": load_pmc_traffic(dom, cfg),
+        "algorithmic_ops_per_launch": model[dom]["ops"], "avg_launch_ms": round(dom_ms, 5),
+        "kernel_hbm": {"workspace_bytes_per_launch": model[dom]["bytes"], "achieved_GBs": round(k_gbs, 2),
+                       "frac": round(k_gbs / HBM_PEAK_GBS, 4)},
         "stage_ms": {k: round(v, 5) for k, v in profile.items()},
         "stage_ms_note": "separate profile pass with events at every stage boundary (adds ~5 us per event)",
-        "frame": {"bytes_per_voxel": nwin * 2 + 3 * sv + 4, "device_ms": round(frame_ms, 4),
-                  "achieved_GBs": round(frame_bytes / (frame_ms * 1e-3) / 1e9, 2),
-                  "frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+        "frame": {"bytes_per_voxel": nwin * 2 + 3 * sv + 4, "algorithmic_bytes": frame_bytes,
+                  "algorithmic_ops": frame_ops, "device_ms": round(frame_ms, 4),
+                  "hbm_GBs": round(f_gbs, 2), "hbm_frac": round(f_gbs / HBM_PEAK_GBS, 4),
+                  "valu_tops": round(f_tops, 3), "valu_frac": round(f_tops / peak_v, 4)},
     }
 
 
@@ -309,14 +358,15 @@ def run_zslab(args, world, rank, local_rank, dev):
         ng = min(zf.z1 + rw, nz) - max(zf.z0 - rw, 0)
         sv = 4 if fp32 else 8
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx, sv),
-                        args.config, (nwin * 2 + 3 * sv + 4) * no * ny * nx, nwin, sv)
+                        args.config, (nwin * 2 + 3 * sv + 4) * no * ny * nx,
+                        frame_ops_per_voxel(rd, rs, rt, rw) * no * ny * nx, nwin, sv)
         roof["frame"]["note"] = "rank 0's slab (output planes %d..%d, input planes %d..%d)" % (
             zf.z0, zf.z1, zf.zi0, zf.zi1)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
             host = synthetic_slab(nwin, nz, ny, nx, 0, sub, seed, dev).cpu().numpy().view(np.uint16)
-            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz)
+            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(vox * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s", "n_gpus": world,
@@ -338,7 +388,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="c3 = configs[2], the largest single-GPU config (the headline); c2 = configs[1]")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
@@ -375,10 +426,9 @@ def main():
 
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
-    frames = synthetic_frames(nt, nz, ny, nx, seed=20260206 + 2 + rank)
-    c = nt // 2
-    win = np.ascontiguousarray(frames[c - rt:c + rt + 1])
-    d_in = torch.from_numpy(win.view(np.int16)).to(dev)
+    # the 2*rt+1 frames around the centre, generated on the device (synthetic_slab: the
+    # SURVEY §8d family; every rank its own seed, i.e. its own output frame)
+    d_in = synthetic_slab(nwin, nz, ny, nx, 0, nz, 20260206 + int(args.config[1:]) + 100 * rank, dev)
     vox = nz * ny * nx
     fp32 = args.precision == "fp32"
     sv = 4 if fp32 else 8
@@ -407,10 +457,13 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = world * vox * args.steps / elapsed / 1e6
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
-                        args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox, nwin, sv)
+                        args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox,
+                        frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(frames, s, t, w, args.cpu_budget)
+            sub = min(cpu_sample_planes(nz, ny, nx, args.cpu_budget), nz)
+            host = d_in[:, :sub].cpu().numpy().view(np.uint16)
+            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
