@@ -1,4 +1,8 @@
-// of3d.hip — MI355X (gfx950) Lucas–Kanade optical flow, fp64 exact mode.
+#pragma once
+// of3d_dev.hpp — device code of libof3d (kernels, pass helpers, geometry constants).
+// Included by every translation unit; the kernel templates are instantiated only in the
+// unit that takes their address (kt_*.hip getters, of3d_host.hip for the small kernels).
+//
 //
 // Re-design (not a port) of the hot path of ScientistRachel/OpticalFlow3D_dev
 // src/Python/calc_flow.py:175-360 (calc_flow3D) and :18-173 (calc_flow2D).
@@ -1420,227 +1424,7 @@ __global__ __launch_bounds__(256) void k_flow_stats(const VT* __restrict__ vx, c
     }
 }
 
-// ---------------------------------------------------------------------------
-// Host side
-// ---------------------------------------------------------------------------
-size_t dtype_size(int dt) {
-    switch (dt) {
-        case OF3D_U8: return 1;
-        case OF3D_U16:
-        case OF3D_I16: return 2;
-        case OF3D_U32:
-        case OF3D_I32:
-        case OF3D_F32: return 4;
-        case OF3D_F64: return 8;
-        default: return 0;
-    }
-}
-
-// scipy NI_Correlate1D symmetry classification: +1, -1, 0
-int symmetry(const double* w, int r) {
-    bool sym = true, anti = true;
-    for (int k = 1; k <= r; ++k) {
-        if (std::fabs(w[r + k] - w[r - k]) > kEps) sym = false;
-        if (std::fabs(w[r + k] + w[r - k]) > kEps) anti = false;
-    }
-    return sym ? 1 : (anti ? -1 : 0);
-}
-
-const char* kStageNames[] = {"grad_xy", "grad_z", "prod_wy", "wx", "wz_solve"};
-constexpr int kStages = 5;
-
-}  // namespace
-
-struct of3d_plan {
-    int ndim = 3;
-    bool rel64 = false;  // OF3D_REL_F64
-    bool fp32 = false;   // OF3D_FP32: passes in float
-    int64_t nz = 1, ny = 1, nx = 1;
-    int rd = 0, rs = 0, rt = 0, rw = 0;
-    int device = 0;
-    int64_t cap_planes = 0;  // planes per workspace field
-    std::vector<double> htaps;  // host copy of half taps (g | d | s | t | w)
-    double* d_taps = nullptr;   // fp64 taps
-    float* d_taps32 = nullptr;  // the same rounded to float (OF3D_FP32)
-    void* X = nullptr;          // 9 fields of the pass type
-    void* Y = nullptr;          // 9 fields
-    size_t fs = 0;        // field stride (elements)
-    hipStream_t stream = nullptr;
-    size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
-    int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
-    size_t k5d_lds = 0;
-    bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
-    bool k2c = true;  // z-march K2 where instantiated (OF3D_K2C=0: k_grad_z)
-    // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
-    const void* k5c = nullptr;
-    size_t k5c_lds = 0;
-    int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
-    // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
-    struct K34Geom {
-        const void* fn = nullptr;
-        int cw = 0, s = 0, tx = 0, nbx = 0;
-        size_t lds = 0;
-    } k34;
-    std::vector<K34Geom> k34_cand;  // geometries that keep >= 8 waves per CU (k34_tune picks)
-    bool host_ev = false;            // host entry: record into ev[]
-    hipEvent_t ev[kStages + 1] = {};
-    int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
-    unsigned timing_mask = (1u << kStages) - 1;  // stages timed (events at their two boundaries)
-    std::vector<hipEvent_t> tev;     // timing_slots * (kStages + 1)
-    int64_t tcount = 0;              // executions recorded since the last of3d_plan_stage_times
-    double stage_ms[kStages] = {};
-    int stages_run = 0;
-    // host-entry staging
-    void* d_in = nullptr;
-    size_t d_in_bytes = 0;
-    void* d_out = nullptr;
-    size_t d_out_bytes = 0;
-};
-
-namespace {
-
-int build_taps(const of3d_taps* t, of3d_plan* p) {
-    if (!t || !t->gauss || !t->deriv || !t->smooth || !t->tderiv || !t->window) return fail("of3d: null taps");
-    if (t->rd < 0 || t->rs < 0 || t->rt < 0 || t->rw < 0) return fail("of3d: negative tap radius");
-    if (t->rd > kMaxR || t->rs > kMaxR || t->rw > kMaxR) return fail("of3d: spatial tap radius exceeds 48");
-    if (2 * t->rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
-    struct {
-        const double* w;
-        int r;
-        int want;
-        const char* name;
-    } f[5] = {{t->gauss, t->rd, 1, "gauss"},
-              {t->deriv, t->rd, -1, "deriv"},
-              {t->smooth, t->rs, 1, "smooth"},
-              {t->tderiv, t->rt, -1, "tderiv"},
-              {t->window, t->rw, 1, "window"}};
-    p->htaps.clear();
-    for (auto& e : f) {
-        if (e.r > 0 && symmetry(e.w, e.r) != e.want)
-            return fail(std::string("of3d: taps '") + e.name + "' do not have the expected (anti)symmetry");
-        for (int k = 0; k <= e.r; ++k) p->htaps.push_back(e.w[e.r - k]);
-    }
-    for (auto& e : f) {  // step-order copies for lds_pass: w[0 .. r-1], then kTapPad zeros
-        for (int q = 0; q < e.r; ++q) p->htaps.push_back(e.w[q]);
-        for (int z = 0; z < kTapPad; ++z) p->htaps.push_back(0.0);
-    }
-    p->rd = t->rd;
-    p->rs = t->rs;
-    p->rt = t->rt;
-    p->rw = t->rw;
-    return 0;
-}
-
-template <typename F>
-DevTaps<F> dev_taps(const of3d_plan* p) {
-    DevTaps<F> d;
-    const F* b;
-    if constexpr (sizeof(F) == 8)
-        b = p->d_taps;
-    else
-        b = p->d_taps32;
-    d.g = b;
-    d.d = d.g + p->rd + 1;
-    d.s = d.d + p->rd + 1;
-    d.t = d.s + p->rs + 1;
-    d.w = d.t + p->rt + 1;
-    d.gr = d.w + p->rw + 1;
-    d.dr = d.gr + p->rd + kTapPad;
-    d.sr = d.dr + p->rd + kTapPad;
-    d.tr = d.sr + p->rs + kTapPad;
-    d.wr = d.tr + p->rt + kTapPad;
-    d.rd = p->rd;
-    d.rs = p->rs;
-    d.rt = p->rt;
-    d.rw = p->rw;
-    return d;
-}
-
-unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
-
-template <typename T, typename F>
-const void* k1_kernel(int rd) {
-    const int nj = (K1_TY + 2 * rd + 3) / 4;
-    if (nj <= 8) return (const void*)k_grad_xy<T, F, 8>;
-    if (nj <= 12) return (const void*)k_grad_xy<T, F, 12>;
-    return (const void*)k_grad_xy<T, F, 16>;
-}
-
-template <typename F>
-const void* k1_kernel_dt(int dtype, int rd) {
-    switch (dtype) {
-        case OF3D_U8: return k1_kernel<uint8_t, F>(rd);
-        case OF3D_U16: return k1_kernel<uint16_t, F>(rd);
-        case OF3D_I16: return k1_kernel<int16_t, F>(rd);
-        case OF3D_U32: return k1_kernel<uint32_t, F>(rd);
-        case OF3D_I32: return k1_kernel<int32_t, F>(rd);
-        case OF3D_F32: return k1_kernel<float, F>(rd);
-        default: return k1_kernel<double, F>(rd);
-    }
-}
-
-template <typename F>
-const void* k0v_kernel_dt(int dtype) {
-    switch (dtype) {
-        case OF3D_U8: return (const void*)k_tderiv_vec<uint8_t, F>;
-        case OF3D_U16: return (const void*)k_tderiv_vec<uint16_t, F>;
-        case OF3D_I16: return (const void*)k_tderiv_vec<int16_t, F>;
-        case OF3D_U32: return (const void*)k_tderiv_vec<uint32_t, F>;
-        case OF3D_I32: return (const void*)k_tderiv_vec<int32_t, F>;
-        case OF3D_F32: return (const void*)k_tderiv_vec<float, F>;
-        default: return (const void*)k_tderiv_vec<double, F>;
-    }
-}
-
-// compile-time-rt K0 instances: u8 / u16 / f32 input, rt 3, 6, 9 (tSig 1, 2, 3)
-template <typename F>
-const void* k0c_fn(int dtype, int rt) {
-    if (const char* e = getenv("OF3D_K0C"); e && e[0] == '0') return nullptr;
-#define OF3D_K0C(T)                                                   \
-    if (rt == 3) return (const void*)k_tderiv_vec_c<T, F, 3>;        \
-    if (rt == 6) return (const void*)k_tderiv_vec_c<T, F, 6>;        \
-    if (rt == 9) return (const void*)k_tderiv_vec_c<T, F, 9>;        \
-    return nullptr;
-    switch (dtype) {
-        case OF3D_U8: { OF3D_K0C(uint8_t) }
-        case OF3D_U16: { OF3D_K0C(uint16_t) }
-        case OF3D_F32: { OF3D_K0C(float) }
-        default: return nullptr;
-    }
-#undef OF3D_K0C
-}
-
-int k0_vec_width(int dtype) {
-    const size_t es = dtype_size(dtype);
-    return es == 1 ? 8 : (es == 8 ? 2 : 4);
-}
-
-template <typename F>
-const void* k0_kernel_dt(int dtype) {
-    switch (dtype) {
-        case OF3D_U8: return (const void*)k_tderiv<uint8_t, F>;
-        case OF3D_U16: return (const void*)k_tderiv<uint16_t, F>;
-        case OF3D_I16: return (const void*)k_tderiv<int16_t, F>;
-        case OF3D_U32: return (const void*)k_tderiv<uint32_t, F>;
-        case OF3D_I32: return (const void*)k_tderiv<int32_t, F>;
-        case OF3D_F32: return (const void*)k_tderiv<float, F>;
-        default: return (const void*)k_tderiv<double, F>;
-    }
-}
-
-template <typename F, typename RelT>
-const void* k5_kernel(int rw) {
-    // NJ = rows per thread of the staged window: ceil((G * R + 2rw) / G)
-    const K5Geom k = k5_geom(rw);
-    if (k.r == 8)
-        return rw <= 16 ? (const void*)k_wz_solve<F, RelT, 12, 8, 8> : (const void*)k_wz_solve<F, RelT, 14, 8, 8>;
-    const int nj = (8 * 4 + 2 * rw + 7) / 8;
-    switch (nj <= 10 ? 10 : (nj <= 12 ? 12 : 16)) {
-        case 10: return (const void*)k_wz_solve<F, RelT, 10, 4, 8>;
-        case 12: return (const void*)k_wz_solve<F, RelT, 12, 4, 8>;
-        default: return (const void*)k_wz_solve<F, RelT, 16, 4, 8>;
-    }
-}
+constexpr int K1C_S = 4;
 
 // LDS-DMA K5: NB window buffers of ceil(H / RPW) 1-KB row groups (RPW = 16 B /
 // sizeof(F) rows); NJ2 = groups per wave.
@@ -1659,910 +1443,4 @@ int k5_dma_nb(int rw) {
     return 3 * buf <= lim ? 3 : (2 * buf <= lim ? 2 : 0);
 }
 
-template <typename F, typename RelT>
-const void* k5_dma_kernel(int rw, int nb) {
-    const K5Geom k = k5_geom(rw);
-    const int nj2 = (k5_groups<F>(rw) + k.g - 1) / k.g;
-#define OF3D_K5D(NJ2, R)                                                     \
-    (nb == 3 ? (const void*)k_wz_solve_dma<F, RelT, NJ2, R, 8, 3>            \
-             : (const void*)k_wz_solve_dma<F, RelT, NJ2, R, 8, 2>)
-    if constexpr (sizeof(F) == 8) {
-        if (k.r == 8) return nj2 <= 6 ? OF3D_K5D(6, 8) : OF3D_K5D(7, 8);  // rw <= 24: nj2 <= 7
-        return nj2 <= 6 ? OF3D_K5D(6, 4) : (nj2 <= 7 ? OF3D_K5D(7, 4) : OF3D_K5D(8, 4));  // rw <= 48: nj2 <= 8
-    } else {
-        if (k.r == 8) return nj2 <= 3 ? OF3D_K5D(3, 8) : OF3D_K5D(4, 8);  // rw <= 24: nj2 <= 4
-        return nj2 <= 3 ? OF3D_K5D(3, 4) : OF3D_K5D(4, 4);                // rw <= 48: nj2 <= 4
-    }
-#undef OF3D_K5D
-}
-
-template <typename F>
-const void* k3_kernel(int np, int rw) {
-    const int tj = (2 * rw + 3) / 4;  // <= 24 for rw <= 48
-    if (np == 9) {
-        if (tj <= 8) return (const void*)k_prod_wy<F, 9, 8>;
-        if (tj <= 12) return (const void*)k_prod_wy<F, 9, 12>;
-        return (const void*)k_prod_wy<F, 9, 24>;
-    }
-    if (tj <= 8) return (const void*)k_prod_wy<F, 5, 8>;
-    if (tj <= 12) return (const void*)k_prod_wy<F, 5, 12>;
-    return (const void*)k_prod_wy<F, 5, 24>;
-}
-
-template <typename F>
-const void* k4_kernel(int nf, int rw) {
-    const int tj = (2 * k4_halo(rw) + 31) / 32;  // <= 3 for rw <= 48
-    if (nf == 9)
-        return tj <= 1 ? (const void*)k_wx<F, 9, 1>
-                       : (tj == 2 ? (const void*)k_wx<F, 9, 2> : (const void*)k_wx<F, 9, 3>);
-    return tj <= 1 ? (const void*)k_wx<F, 5, 1> : (tj == 2 ? (const void*)k_wx<F, 5, 2> : (const void*)k_wx<F, 5, 3>);
-}
-
-// K1c instances: input dtypes u8 / u16 / f32, (rd, rs) = (3, 1), (6, 2), (9, 3) (xyzSig 1, 2, 3);
-// others use k_grad_xy.
-constexpr int K1C_S = 4;
-template <typename F>
-const void* k1c_fn(int dtype, int rd, int rs) {
-#define OF3D_K1C(T)                                                                           \
-    if (rd == 3 && rs == 1) return (const void*)k_grad_xy_c<T, F, 3, 1, K1C_S>;               \
-    if (rd == 6 && rs == 2) return (const void*)k_grad_xy_c<T, F, 6, 2, K1C_S>;               \
-    if (rd == 9 && rs == 3) return (const void*)k_grad_xy_c<T, F, 9, 3, K1C_S>;               \
-    return nullptr;
-    switch (dtype) {
-        case OF3D_U8: { OF3D_K1C(uint8_t) }
-        case OF3D_U16: { OF3D_K1C(uint16_t) }
-        case OF3D_F32: { OF3D_K1C(float) }
-        default: return nullptr;
-    }
-#undef OF3D_K1C
-}
-
-// K34 instances: W radii with a compiled register ring (others use K3 + K4)
-template <typename F, int NP>
-const void* k34_fn(int rw, int s, int rb) {
-#define OF3D_K34(RW, SA, SB)                                    \
-    case RW:                                                    \
-        if (s == SA) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, RW, SA>;                                     \
-        if (s == SB) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, RW, SB>;                                     \
-        return nullptr;
-    switch (rw) {
-        OF3D_K34(12, 16, 8)
-        OF3D_K34(15, 16, 8)
-        OF3D_K34(21, 8, 4)  // register ring of 44-48 rows: shorter tiles
-        default: return nullptr;
-    }
-#undef OF3D_K34
-}
-
-// K34 geometry: waves per block nw in {1, 2, 4} (staged columns cw = 64 nw,
-// tx = (cw - 2rw) & ~3 outputs) and tile rows S.  Fewest staged lanes over the
-// row (halo + idle lanes) among the shapes that keep >= 8 waves per CU resident
-// (LDS and registers from the occupancy API), ties to the higher occupancy.
-template <typename F>
-int k34_setup(of3d_plan* p, int np) {
-    p->k34 = {};
-    p->k34_cand.clear();
-    if (const char* e = getenv("OF3D_K34"); e && e[0] == '0') return 0;
-    const int rw = p->rw, nx = (int)p->nx;
-    const size_t es = sizeof(F);
-    if ((size_t)p->ny * p->nx * es > 0x7fffffffu) return 0;  // 32-bit buffer offsets within a plane
-    long best_lanes = 0;
-    int best_waves = 0;
-    const char* env_nw = getenv("OF3D_K34_NW");  // overrides (experiments)
-    const char* env_s = getenv("OF3D_K34_S");
-    for (int s : {16, 8, 4}) {
-        if (env_s && atoi(env_s) != s) continue;
-      for (int rb : {4, 2}) {
-        if (getenv("OF3D_K34_RB") && atoi(getenv("OF3D_K34_RB")) != rb) continue;
-        const void* fn = np == 9 ? k34_fn<F, 9>(rw, s, rb) : k34_fn<F, 5>(rw, s, rb);
-        if (!fn) continue;
-        for (int nw : {1, 2, 3, 4, 8}) {  // launch bound 512
-            // blocks of 5-7 waves measured as if one block per CU fitted (c2: nw 5, 6, 7 all
-            // ~300 us vs 242 us at nw 2); keep whole-SIMD multiples
-            if (env_nw ? atoi(env_nw) != nw : nw == 8) continue;
-            const int cw = 64 * nw, tx = (cw - 2 * rw) & ~3;  // tx: whole phase-B items
-            if (tx < 8) continue;
-            const int nbx = (nx + tx - 1) / tx;
-            const size_t lds = (size_t)2 * k34_tile(s, cw + 1) * es;  // two W-y tiles
-            if (lds > 160 * 1024) continue;
-            OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            int nb = 0;
-            OF3D_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, cw, lds));
-            const int waves = nb * nw;
-            if (waves == 0) continue;
-            const long lanes = (long)(nbx - 1) * cw + 64 * ((nx - (nbx - 1) * tx + 2 * rw + 63) / 64);
-            const bool ok = waves >= 8, best_ok = best_waves >= 8;
-            if (ok) {
-                OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                p->k34_cand.push_back({fn, cw, s, tx, nbx, lds});
-            }
-            const bool better = !p->k34.fn || (ok && !best_ok) ||
-                                (ok == best_ok && (ok ? (lanes < best_lanes || (lanes == best_lanes && waves > best_waves))
-                                                      : waves > best_waves));
-            if (better) {
-                p->k34.fn = fn;
-                p->k34.cw = cw;
-                p->k34.s = s;
-                p->k34.tx = tx;
-                p->k34.nbx = nbx;
-                p->k34.lds = lds;
-                best_lanes = lanes;
-                best_waves = waves;
-            }
-        }
-      }
-    }
-    if (p->k34.fn)
-        OF3D_HIP(hipFuncSetAttribute(p->k34.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if (getenv("OF3D_VERBOSE") && p->k34.fn)
-        fprintf(stderr, "of3d: K34 cw=%d s=%d tx=%d nbx=%d lds=%zu lanes=%ld waves/CU=%d\n", p->k34.cw, p->k34.s,
-                p->k34.tx, p->k34.nbx, p->k34.lds, best_lanes, best_waves);
-    return 0;
-}
-
-// K5c instances (window radii with a compiled pass; others use k_wz_solve_dma)
-template <typename F, typename RelT>
-const void* k5c_fn(int rw, int nb, int r) {
-#define OF3D_K5C(RW) \
-    case RW:                                                                                            \
-        if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 4> : nullptr;            \
-        return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8> : (const void*)k_wz_solve_c<F, RelT, RW, 2, 8>;
-    switch (rw) {
-        OF3D_K5C(12)
-        OF3D_K5C(15)
-        OF3D_K5C(21)
-        default: return nullptr;
-    }
-#undef OF3D_K5C
-}
-
-template <typename F>
-int k5c_setup(of3d_plan* p) {
-    p->k5c = nullptr;
-    if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
-    if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
-    const char* er = getenv("OF3D_K5C_R");
-    const int r = er ? atoi(er) : 8;
-    const size_t buf = (size_t)k5c_groups<F>(p->rw, r) * 1024;
-    const int nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;  // two blocks per CU
-    const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r) : k5c_fn<F, float>(p->rw, nb, r);
-    if (!fn) return 0;
-    p->k5c_r = r;
-    p->k5c_lds = nb * buf;
-    OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
-    p->k5c = fn;
-    return 0;
-}
-
-// One K34 launch over ng planes of nf products.  Rows are cut into chunks of >= 32
-// rows (each chunk re-reads 2 rw halo rows) until there are >= 4096 blocks (measured
-// 2-3 % faster than 2048 on c2/c3: shorter tail); blocks of one group share an XCD: all row chunks of a plane when there are
-// planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
-template <typename K, typename F>
-hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
-                      hipStream_t s) {
-    const int nyb_max = std::max(1, ny / 32);
-    static const long target = 4L * 256 * 2 * (getenv("OF3D_K34_NYBX") ? atol(getenv("OF3D_K34_NYBX")) : 2);
-    int nyb = 1;
-    while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
-    int nyc = (ny + nyb - 1) / nyb;
-    nyc = (nyc + k.s - 1) / k.s * k.s;
-    nyb = (ny + nyc - 1) / nyc;
-    int cpg = ng >= 32 ? nyb : 1;
-    int groups = ng * ((nyb + cpg - 1) / cpg);
-    const int mb = cpg * nf * k.nbx;
-    const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
-    int tx = k.tx, nbx = k.nbx;
-    void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&hw,
-                    (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
-    return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.cw), args, k.lds, s);
-}
-
-// K34 autotune at plan creation: every candidate geometry of k34_setup timed on the
-// plan's own workspace (whole volume, contents irrelevant to the time), the fastest kept.
-// Measured picks differ by config (c2: 2-wave blocks; c3: 4-wave blocks, 4-row tiles).
-template <typename F>
-int k34_tune(of3d_plan* p) {
-    if (p->k34_cand.size() <= 1) return 0;
-    const int nf = p->ndim == 3 ? 9 : 5, ng = (int)std::min<int64_t>(p->nz, p->cap_planes);
-    F* G = (F*)(p->ndim == 3 ? p->Y : p->X);
-    F* P = (F*)(p->ndim == 3 ? p->X : p->Y);
-    const F* hw = dev_taps<F>(p).w;
-    hipEvent_t e0, e1;
-    OF3D_HIP(hipEventCreate(&e0));
-    OF3D_HIP(hipEventCreate(&e1));
-    // the heuristic pick (k34_setup) stays unless another shape is >= 3 % faster: stable
-    // choices from run to run (candidates within noise of each other otherwise flip)
-    size_t h0 = 0;
-    for (size_t i = 0; i < p->k34_cand.size(); ++i)
-        if (p->k34_cand[i].fn == p->k34.fn && p->k34_cand[i].cw == p->k34.cw) h0 = i;
-    std::swap(p->k34_cand[0], p->k34_cand[h0]);
-    float best = 1e30f;
-    size_t bi = 0;
-    for (size_t i = 0; i < p->k34_cand.size(); ++i) {
-        const auto& k = p->k34_cand[i];
-        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));  // warm
-        OF3D_HIP(hipEventRecord(e0, p->stream));
-        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
-        OF3D_HIP(hipEventRecord(e1, p->stream));
-        OF3D_HIP(hipEventSynchronize(e1));
-        float ms = 0.f;
-        OF3D_HIP(hipEventElapsedTime(&ms, e0, e1));
-        if (i == 0 ? true : ms < 0.97f * best) best = ms, bi = i;
-    }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    p->k34 = p->k34_cand[bi];
-    if (getenv("OF3D_VERBOSE"))
-        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d (%.3f ms)\n", p->k34_cand.size(),
-                p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, best);
-    return 0;
-}
-
-template <typename F>
-int set_attrs_t(of3d_plan* p) {
-    const size_t e = sizeof(F);
-    p->k1_lds = (size_t)(2 * (K1_TY + 2 * p->rd) + 3 * K1_TY) * 64 * e;
-    p->k2_lds = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * e;
-    p->k3_lds = (size_t)(K3_STEP + 2 * p->rw) * 64 * e;
-    p->k4_lds = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * e;
-    p->k5_lds = (size_t)2 * (k5_geom(p->rw).g * k5_geom(p->rw).r + 2 * p->rw) * 64 * e;
-    const size_t lim = 160 * 1024;
-    if (p->k3_lds > lim || p->k4_lds > lim || p->k5_lds > lim) return fail("of3d: wSig too large for the LDS tiles");
-    auto attr = [&](const void* k, size_t b) -> int {
-        OF3D_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)b));
-        return 0;
-    };
-    int rc = 0;
-    for (int dt = OF3D_U8; dt <= OF3D_F64; ++dt) rc |= attr(k1_kernel_dt<F>(dt, p->rd), p->k1_lds);
-    rc |= attr((const void*)k_grad_z<F>, p->k2_lds);
-    rc |= attr(k3_kernel<F>(9, p->rw), p->k3_lds) | attr(k3_kernel<F>(5, p->rw), p->k3_lds);
-    rc |= attr(k4_kernel<F>(9, p->rw), p->k4_lds) | attr(k4_kernel<F>(5, p->rw), p->k4_lds);
-    rc |= attr(k5_kernel<F, float>(p->rw), p->k5_lds) | attr(k5_kernel<F, double>(p->rw), p->k5_lds);
-    constexpr int epl = 16 / (int)sizeof(F);
-    p->k5_nb = (p->nx % epl == 0) ? k5_dma_nb<F>(p->rw) : 0;
-    if (p->k5_nb) {
-        p->k5d_lds = (size_t)p->k5_nb * k5_groups<F>(p->rw) * 1024;
-        rc |= attr(k5_dma_kernel<F, float>(p->rw, p->k5_nb), p->k5d_lds) |
-              attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
-    }
-    if (rc) return -1;
-    if (const char* e = getenv("OF3D_K1C"); e && e[0] == '0') p->k1c = false;
-    if (const char* e = getenv("OF3D_K2C"); e && e[0] == '0') p->k2c = false;
-    for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32})
-        if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
-            OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if (k5c_setup<F>(p)) return -1;
-    return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
-}
-
-int set_attrs(of3d_plan* p) {
-    if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
-    return p->fp32 ? set_attrs_t<float>(p) : set_attrs_t<double>(p);
-}
-
-struct Ranges {
-    int64_t zo0, zo1, zg0, zg1, zb0, zb1;
-};
-
-Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
-    Ranges r;
-    r.zo0 = zo0;
-    r.zo1 = zo1;
-    if (p->ndim == 2) {
-        r.zg0 = r.zb0 = 0;
-        r.zg1 = r.zb1 = 1;
-        return r;
-    }
-    r.zg0 = std::max<int64_t>(zo0 - p->rw, 0);
-    r.zg1 = std::min<int64_t>(zo1 + p->rw, p->nz);
-    r.zb0 = std::max<int64_t>(r.zg0 - p->rd, 0);
-    r.zb1 = std::min<int64_t>(r.zg1 + p->rd, p->nz);
-    return r;
-}
-
-template <typename F>
-int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx_,
-          void* vy_, void* vz_, void* rel, hipStream_t s) {
-    F* vx = (F*)vx_;
-    F* vy = (F*)vy_;
-    F* vz = (F*)vz_;
-    F* X = (F*)p->X;
-    F* Y = (F*)p->Y;
-    if (!p) return fail("of3d: null plan");
-    if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
-    const Ranges R = ranges(p, zo0, zo1);
-    if (R.zb1 - R.zb0 > p->cap_planes) return fail("of3d: output range exceeds the plan's workspace");
-    if (frame_z0 > R.zb0) return fail("of3d: frames do not hold the stencil halo planes");
-    if (dtype_size(dtype) == 0) return fail("of3d: unsupported dtype");
-    const int ny = (int)p->ny, nx = (int)p->nx;
-    Frames fr{};
-    for (int i = 0; i < 2 * p->rt + 1; ++i) {
-        if (!d_frames[i]) return fail("of3d: null frame pointer");
-        fr.p[i] = d_frames[i];
-    }
-    const DevTaps<F> tp = dev_taps<F>(p);
-    const size_t fs = p->fs;
-    const int nb = (int)(R.zb1 - R.zb0), ng = (int)(R.zg1 - R.zg0), no = (int)(R.zo1 - R.zo0);
-    hipEvent_t* evs = p->host_ev ? p->ev
-                      : (p->timing_slots ? &p->tev[(size_t)(p->tcount % p->timing_slots) * (kStages + 1)] : nullptr);
-    // boundary i opens stage i and closes stage i-1; untimed stages get no events
-    // (every event is a barrier packet between kernels: a few microseconds each)
-    const unsigned bmask = p->host_ev ? ~0u : (p->timing_mask | (p->timing_mask << 1));
-#define OF3D_MARK(i) \
-    do { \
-        if (evs && ((bmask >> (i)) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s)); \
-    } while (0)
-    OF3D_MARK(0);
-    // K0 + K1 — frames equally spaced (one stack) are addressed by stride
-    {
-        const size_t es = dtype_size(dtype);
-        long long fstride = 0;
-        const int nwin = 2 * p->rt + 1;
-        if (nwin > 1) {
-            const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
-            bool eq = d > 0 && d % (long long)es == 0;
-            for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
-            if (eq) fstride = d / (long long)es;
-        }
-        const size_t plane = (size_t)ny * nx;
-        size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)nb * plane;
-        int rt_arg = p->rt;
-        F* D0 = Y;  // Y field 0 is free until K2 writes it
-        const int V = k0_vec_width(dtype);
-        const size_t vb = (size_t)V * es;
-        bool vec = off0 % V == 0 && n % V == 0;
-        for (int i = 0; vec && i < nwin; ++i) vec = ((uintptr_t)d_frames[i] % vb) == 0;
-        if (vec) {
-            size_t ng = n / V;
-            const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
-            void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
-            const void* k0 = k0c_fn<F>(dtype, p->rt);
-            if (k0) {
-                void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
-                OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, s));
-            } else {
-                OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
-            }
-        } else {
-            const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
-            void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
-                            (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
-        }
-        {
-            const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
-            const F* D0c = D0;
-            int need_b4 = p->ndim == 3, nb_arg = nb;
-            dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
-            void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
-                            (void*)&X, (void*)&fs, (void*)&need_b4};
-            // (32-bit buffer offsets within a plane: planes up to 2 GiB)
-            const bool k1c_ok = p->k1c && (size_t)ny * nx * sizeof(F) <= 0x7fffffffu;
-            const void* k1c = k1c_ok ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
-            if (k1c) {
-                // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
-                static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
-                static const int nyc_env = getenv("OF3D_K1C_NYC") ? atoi(getenv("OF3D_K1C_NYC")) : 32;
-                const int cw = cw_env ? cw_env : (nx <= 256 ? 128 : 256);  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
-                int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
-                int nyc = std::min(ny, nyc_env), nyb;
-                while (true) {
-                    nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
-                    nyb = (ny + nyc - 1) / nyc;
-                    if ((long)nb * nyb * nbx <= 8192 || nyc >= ny) break;
-                    nyc *= 2;
-                }
-                const size_t lds = (size_t)6 * k34_tile(K1C_S, cw + 1) * sizeof(F);
-                const unsigned blocks = (unsigned)((long)nb * nyb * nbx);
-                void* cargs[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&tp, (void*)&X,
-                                 (void*)&fs, (void*)&need_b4, (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb};
-                OF3D_HIP(hipLaunchKernel(k1c, dim3(blocks), dim3(cw), cargs, lds, s));
-            } else {
-                OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
-            }
-        }
-    }
-    OF3D_MARK(1);
-    const F* G;
-    if (p->ndim == 3) {
-        const void* k2c = nullptr;
-        if (p->k2c) {
-            if (p->rd == 6 && p->rs == 2) k2c = (const void*)k_grad_z_c<F, 6, 2>;
-            if (p->rd == 3 && p->rs == 1) k2c = (const void*)k_grad_z_c<F, 3, 1>;
-        }
-        if (k2c) {
-            // z march: 256 columns per block, chunks of >= 32 planes (2 rd halo planes re-read per chunk)
-            const int plane = ny * nx;
-            int zc = std::min(ng, 32);
-            while ((long)cdiv(plane, 256) * cdiv(ng, zc) > 8192 && zc < ng) zc *= 2;
-            const F* Bc = X;
-            // input planes clamp at zb1 (= nz at the top edge): see the K5 launch
-            int zb0 = (int)R.zb0, zg0 = (int)R.zg0, ngz = ng, nzz = (int)R.zb1;
-            void* args[] = {(void*)&Bc, (void*)&zb0, (void*)&Y, (void*)&zg0, (void*)&ngz, (void*)&nzz, (void*)&plane,
-                            (void*)&fs, (void*)&tp, (void*)&zc};
-            OF3D_HIP(hipLaunchKernel(k2c, dim3(cdiv(plane, 256), cdiv(ng, zc)), dim3(256), args, 0, s));
-        } else {
-            dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
-            hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, s, X, (int)R.zb0, Y, (int)R.zg0, ng,
-                               (int)R.zb1, ny, nx, fs, tp);
-            OF3D_HIP(hipGetLastError());
-        }
-        G = Y;
-    } else {
-        G = X;
-    }
-    OF3D_MARK(2);
-    F* P = p->ndim == 3 ? X : Y;
-    F* Q = p->ndim == 3 ? Y : X;  // W-xy result (K4), or P when K34 writes it (G lives in Q's buffer)
-    if (p->k34.fn) Q = P;
-    const int nf = p->ndim == 3 ? 9 : 5;
-    if (p->k34.fn) {
-        // fused products + W y + W x (stage "prod_wy"; stage "wx" stays empty)
-        OF3D_HIP(launch_k34(p->k34, G, P, ng, nf, ny, nx, fs, tp.w, s));
-        OF3D_MARK(3);
-    } else {
-    {
-        dim3 g(cdiv(nx, 64), 1, ng * nf);
-        int rw_arg = p->rw;
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
-                        (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
-    }
-    OF3D_MARK(3);
-    {
-        dim3 g(1, cdiv(ny, K4_ROWS), ng * nf);
-        int rw_arg = p->rw;
-        const F* Pc = P;
-        void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
-                        (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
-    }
-    }
-    OF3D_MARK(4);
-    if (p->ndim == 3) {
-        const K5Geom kg = k5_geom(p->rw);
-        dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
-        int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
-        // window planes clamp at zg1 (= nz at the volume's top edge): the rows a block
-        // loads past its last output plane stay inside the workspace's W-xy planes
-        int zq1 = (int)R.zg1;
-        const F* Qc = Q;
-        void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                        (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-        if (p->k5c) {
-            dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
-            void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                             (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-            OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, s));
-        } else if (p->k5_nb) {
-            const void* k5 = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
-            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
-        } else {
-            const void* k5 = p->rel64 ? k5_kernel<F, double>(p->rw) : k5_kernel<F, float>(p->rw);
-            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5_lds, s));
-        }
-    } else {
-        const int n = ny * nx;
-        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (F*)rel);
-    }
-    OF3D_HIP(hipGetLastError());
-    OF3D_MARK(5);
-    p->stages_run = kStages;
-    if (!p->host_ev && p->timing_slots) ++p->tcount;
-#undef OF3D_MARK
-    return 0;
-}
-
-int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx,
-        void* vy, void* vz, void* rel, hipStream_t s) {
-    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s)
-                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
-}
-
-int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
-                int device, int64_t max_out_planes) {
-    if (!out) return fail("of3d: null plan pointer");
-    *out = nullptr;
-    if ((mode & ~(OF3D_REL_F64 | OF3D_FP32)) != OF3D_FP64_EXACT) return fail("of3d: unsupported mode");
-    if (ndim != 2 && ndim != 3) return fail("of3d: ndim must be 2 or 3");
-    if (ndim == 2 && nz != 1) return fail("of3d: 2D plans need nz == 1");
-    if (nz < 1 || ny < 1 || nx < 1) return fail("of3d: empty volume");
-    if (ny * nx > (int64_t)INT32_MAX || nz > 65535) return fail("of3d: volume too large for one plan");
-    std::unique_ptr<of3d_plan> p(new of3d_plan);
-    p->ndim = ndim;
-    p->rel64 = (mode & OF3D_REL_F64) != 0;
-    p->fp32 = (mode & OF3D_FP32) != 0;
-    p->nz = nz;
-    p->ny = ny;
-    p->nx = nx;
-    p->device = device;
-    if (build_taps(taps, p.get())) return -1;
-    OF3D_HIP(hipSetDevice(device));
-    if (set_attrs(p.get())) return -1;
-    int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
-    p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
-    p->fs = (size_t)p->cap_planes * ny * nx;
-    OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
-    OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
-    {
-        std::vector<float> h32(p->htaps.begin(), p->htaps.end());  // round-to-nearest, as numpy's astype
-        OF3D_HIP(hipMalloc(&p->d_taps32, h32.size() * sizeof(float)));
-        OF3D_HIP(hipMemcpy(p->d_taps32, h32.data(), h32.size() * sizeof(float), hipMemcpyHostToDevice));
-    }
-    const size_t es = p->fp32 ? sizeof(float) : sizeof(double);
-    OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * es));
-    OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * es));
-    OF3D_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
-        OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
-        OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
-        if ((p->fp32 ? k34_tune<float>(p.get()) : k34_tune<double>(p.get()))) return -1;
-    }
-    for (auto& e : p->ev) OF3D_HIP(hipEventCreate(&e));
-    *out = p.release();
-    return 0;
-}
-
-void plan_free(of3d_plan* p) {
-    if (!p) return;
-    (void)hipSetDevice(p->device);
-    if (p->stream) (void)hipStreamSynchronize(p->stream);
-    (void)hipFree(p->d_taps);
-    (void)hipFree(p->d_taps32);
-    (void)hipFree(p->X);
-    (void)hipFree(p->Y);
-    (void)hipFree(p->d_in);
-    (void)hipFree(p->d_out);
-    for (auto& e : p->ev)
-        if (e) (void)hipEventDestroy(e);
-    for (auto e : p->tev) (void)hipEventDestroy(e);
-    if (p->stream) (void)hipStreamDestroy(p->stream);
-    delete p;
-}
-
-// ---- host-entry plan cache (one plan per thread's last shape) ------------
-struct CacheKey {
-    int ndim, device, mode;
-    int64_t nz, ny, nx;
-    std::vector<double> taps;
-    std::vector<int> radii;
-    bool operator==(const CacheKey& o) const {
-        return ndim == o.ndim && device == o.device && mode == o.mode && nz == o.nz && ny == o.ny && nx == o.nx && taps == o.taps &&
-               radii == o.radii;
-    }
-};
-
-std::mutex g_cache_mu;
-struct CacheEntry {
-    CacheKey key;
-    of3d_plan* plan = nullptr;
-};
-std::vector<CacheEntry> g_cache;  // small LRU
-
-CacheKey make_key(int ndim, int device, int mode, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* t) {
-    CacheKey k{ndim, device, mode, nz, ny, nx, {}, {t->rd, t->rs, t->rt, t->rw}};
-    auto add = [&](const double* w, int r) { k.taps.insert(k.taps.end(), w, w + 2 * r + 1); };
-    add(t->gauss, t->rd);
-    add(t->deriv, t->rd);
-    add(t->smooth, t->rs);
-    add(t->tderiv, t->rt);
-    add(t->window, t->rw);
-    return k;
-}
-
-int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, int64_t ny, int64_t nx,
-              const of3d_taps* taps, int mode, int device, double* vx, double* vy, double* vz, void* rel,
-              of3d_perf* perf) {
-    const auto t0 = std::chrono::steady_clock::now();
-    if (!images || !vx || !vy || !rel || (ndim == 3 && !vz)) return fail("of3d: null buffer");
-    if (!taps) return fail("of3d: null taps");
-    if (mode & OF3D_FP32) return fail("of3d: OF3D_FP32 is a plan mode (float outputs); use of3d_plan_*");
-    const size_t es = dtype_size(dtype);
-    if (!es) return fail("of3d: unsupported dtype");
-    if (nt < 1 || !(nt & 1)) return fail("of3d: nt must be odd");
-    const int64_t c = nt / 2;  // ceil(Nt/2)-1 for odd Nt (calc_flow.py:223)
-    const int rt = taps->rt;
-    if (taps->rt < 0 || 2 * rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
-    std::lock_guard<std::mutex> lk(g_cache_mu);
-    CacheKey key = make_key(ndim, device, mode, nz, ny, nx, taps);
-    of3d_plan* p = nullptr;
-    for (size_t i = 0; i < g_cache.size(); ++i)
-        if (g_cache[i].key == key) {
-            p = g_cache[i].plan;
-            std::rotate(g_cache.begin(), g_cache.begin() + i, g_cache.begin() + i + 1);
-            break;
-        }
-    if (!p) {
-        if (plan_create(&p, ndim, nz, ny, nx, taps, mode, device, 0)) return -1;
-        g_cache.insert(g_cache.begin(), CacheEntry{key, p});
-        while (g_cache.size() > 2) {
-            plan_free(g_cache.back().plan);
-            g_cache.pop_back();
-        }
-    }
-    OF3D_HIP(hipSetDevice(device));
-    const size_t vox = (size_t)nz * ny * nx;
-    // Only frames c-rt..c+rt enter the result (time indices clamped to [0,nt)).
-    const int nwin = 2 * rt + 1;
-    const size_t in_bytes = (size_t)nwin * vox * es;
-    if (p->d_in_bytes < in_bytes) {
-        (void)hipFree(p->d_in);
-        p->d_in = nullptr;
-        OF3D_HIP(hipMalloc(&p->d_in, in_bytes));
-        p->d_in_bytes = in_bytes;
-    }
-    const size_t rel_es = (ndim == 3 && !(mode & OF3D_REL_F64)) ? sizeof(float) : sizeof(double);
-    const size_t out_bytes = vox * (3 * sizeof(double) + rel_es);
-    if (p->d_out_bytes < out_bytes) {
-        (void)hipFree(p->d_out);
-        p->d_out = nullptr;
-        OF3D_HIP(hipMalloc(&p->d_out, out_bytes));
-        p->d_out_bytes = out_bytes;
-    }
-    hipStream_t s = p->stream;
-    hipEvent_t e0 = p->ev[0], e1 = p->ev[1];
-    const void* dptr[kMaxT];
-    // distinct frames needed, uploaded once each
-    std::vector<int64_t> src(nwin);
-    for (int i = 0; i < nwin; ++i) src[i] = std::min<int64_t>(std::max<int64_t>(c - rt + i, 0), nt - 1);
-    for (int i = 0; i < nwin; ++i) {
-        char* dst = (char*)p->d_in + (size_t)i * vox * es;
-        dptr[i] = dst;
-        OF3D_HIP(hipMemcpyAsync(dst, (const char*)images + (size_t)src[i] * vox * es, vox * es, hipMemcpyHostToDevice, s));
-    }
-    OF3D_HIP(hipStreamSynchronize(s));
-    const auto t1 = std::chrono::steady_clock::now();
-    double* dvx = (double*)p->d_out;
-    double* dvy = dvx + vox;
-    double* dvz = dvy + vox;
-    void* drel = (void*)(dvz + vox);
-    p->host_ev = true;
-    int rc = run(p, dptr, dtype, 0, 0, nz, dvx, dvy, ndim == 3 ? dvz : nullptr, drel, s);
-    p->host_ev = false;
-    if (rc) return rc;
-    OF3D_HIP(hipStreamSynchronize(s));
-    float kms = 0.f;
-    OF3D_HIP(hipEventElapsedTime(&kms, p->ev[0], p->ev[kStages]));
-    for (int i = 0; i < kStages; ++i) {
-        float m = 0.f;
-        (void)hipEventElapsedTime(&m, p->ev[i], p->ev[i + 1]);
-        p->stage_ms[i] = m;
-    }
-    (void)e0;
-    (void)e1;
-    const auto t2 = std::chrono::steady_clock::now();
-    OF3D_HIP(hipMemcpyAsync(vx, dvx, vox * sizeof(double), hipMemcpyDeviceToHost, s));
-    OF3D_HIP(hipMemcpyAsync(vy, dvy, vox * sizeof(double), hipMemcpyDeviceToHost, s));
-    if (ndim == 3) OF3D_HIP(hipMemcpyAsync(vz, dvz, vox * sizeof(double), hipMemcpyDeviceToHost, s));
-    OF3D_HIP(hipMemcpyAsync(rel, drel, vox * rel_es, hipMemcpyDeviceToHost, s));
-    OF3D_HIP(hipStreamSynchronize(s));
-    const auto t3 = std::chrono::steady_clock::now();
-    if (perf) {
-        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-        perf->ms_h2d = ms(t0, t1);
-        perf->ms_kernels = kms;
-        perf->ms_d2h = ms(t2, t3);
-        perf->ms_total = ms(t0, t3);
-    }
-    return 0;
-}
-
 }  // namespace
-
-// ---------------------------------------------------------------------------
-// Bounded-footprint copy (of3d_copy_async): 16-byte lanes, non-temporal
-// stores, grid-stride over at most max_blocks workgroups; byte tail by block 0.
-// ---------------------------------------------------------------------------
-namespace {
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n16,
-                                              const unsigned char* __restrict__ tsrc, unsigned char* __restrict__ tdst,
-                                              int tail) {
-    const size_t st = (size_t)gridDim.x * 256;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += st)
-        __builtin_nontemporal_store(src[i], &dst[i]);
-    if (blockIdx.x == 0 && (int)threadIdx.x < tail) tdst[threadIdx.x] = tsrc[threadIdx.x];
-}
-
-__global__ __launch_bounds__(256) void k_copy_bytes(const unsigned char* __restrict__ src,
-                                                    unsigned char* __restrict__ dst, size_t n) {
-    const size_t st = (size_t)gridDim.x * 256;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) dst[i] = src[i];
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------
-// C-ABI
-// ---------------------------------------------------------------------------
-extern "C" {
-
-int of3d_version(void) { return OF3D_VERSION; }
-
-const char* of3d_last_error(void) { return g_err.c_str(); }
-
-int of3d_device_count(void) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
-    return n;
-}
-
-int of3d_flow3d(const void* images, int dtype, int64_t nt, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps,
-                int mode, int device, double* vx, double* vy, double* vz, void* rel, of3d_perf* perf) {
-    return host_flow(3, images, dtype, nt, nz, ny, nx, taps, mode, device, vx, vy, vz, rel, perf);
-}
-
-int of3d_flow2d(const void* images, int dtype, int64_t nt, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
-                int device, double* vx, double* vy, double* rel, of3d_perf* perf) {
-    return host_flow(2, images, dtype, nt, 1, ny, nx, taps, mode, device, vx, vy, nullptr, rel, perf);
-}
-
-int of3d_plan_create(of3d_plan** plan, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
-                     int device, int64_t max_out_planes) {
-    return plan_create(plan, ndim, nz, ny, nx, taps, mode, device, max_out_planes);
-}
-
-int of3d_plan_destroy(of3d_plan* plan) {
-    plan_free(plan);
-    return 0;
-}
-
-size_t of3d_plan_workspace_bytes(const of3d_plan* p) {
-    return p ? 18 * p->fs * (p->fp32 ? sizeof(float) : sizeof(double)) : 0;
-}
-
-int of3d_plan_input_range(const of3d_plan* p, int64_t zo0, int64_t zo1, int64_t* zi0, int64_t* zi1) {
-    if (!p || !zi0 || !zi1) return fail("of3d: null argument");
-    if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
-    const Ranges r = ranges(p, zo0, zo1);
-    *zi0 = r.zb0;
-    *zi1 = r.zb1;
-    return 0;
-}
-
-int of3d_plan_execute(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1,
-                      void* vx, void* vy, void* vz, void* rel, void* stream) {
-    if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
-    OF3D_HIP(hipSetDevice(p->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
-    return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
-}
-
-int of3d_plan_set_timing(of3d_plan* p, int slots) {
-    if (!p) return fail("of3d: null plan");
-    if (slots < 0 || slots > 4096) return fail("of3d: timing slots must be in [0, 4096]");
-    OF3D_HIP(hipSetDevice(p->device));
-    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
-    for (auto e : p->tev) (void)hipEventDestroy(e);
-    p->tev.assign((size_t)slots * (kStages + 1), nullptr);
-    for (auto& e : p->tev) OF3D_HIP(hipEventCreate(&e));
-    p->timing_slots = slots;
-    p->tcount = 0;
-    return 0;
-}
-
-int of3d_plan_set_timing_mask(of3d_plan* p, unsigned mask) {
-    if (!p) return fail("of3d: null plan");
-    mask &= (1u << kStages) - 1;
-    if (!mask) return fail("of3d: timing mask selects no stage");
-    OF3D_HIP(hipSetDevice(p->device));
-    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
-    p->timing_mask = mask;
-    p->tcount = 0;
-    return 0;
-}
-
-int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
-    if (!p || !ms) return fail("of3d: null argument");
-    if (!p->timing_slots) return fail("of3d: timing not enabled on this plan");
-    const int64_t n = std::min<int64_t>(p->tcount, p->timing_slots);
-    if (n == 0) return fail("of3d: no timed executions since the last read");
-    const int m = std::min(cap, kStages);
-    std::vector<double> acc(kStages, 0.0);
-    for (int64_t j = 0; j < n; ++j) {
-        hipEvent_t* e = &p->tev[(size_t)j * (kStages + 1)];
-        int last = kStages;
-        while (!((p->timing_mask >> (last - 1)) & 1u)) --last;  // closing boundary of the last timed stage
-        OF3D_HIP(hipEventSynchronize(e[last]));
-        for (int i = 0; i < kStages; ++i) {
-            if (!((p->timing_mask >> i) & 1u)) continue;
-            float t = 0.f;
-            OF3D_HIP(hipEventElapsedTime(&t, e[i], e[i + 1]));
-            acc[i] += t;
-        }
-    }
-    for (int i = 0; i < m; ++i) ms[i] = ((p->timing_mask >> i) & 1u) ? acc[i] / (double)n : -1.0;
-    if (p->k34.fn && m > 3) ms[3] = -1.0;  // fused K34: "prod_wy" holds W x too, "wx" is empty
-    p->tcount = 0;
-    return m;
-}
-
-const char* of3d_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
-
-int of3d_dma_copy(void* const* dst, const void* const* src, const size_t* bytes, int n) {
-    if (n <= 0) return 0;
-    if (!dst || !src || !bytes) return fail("of3d: null argument");
-    static std::once_flag once;
-    static hsa_status_t init = HSA_STATUS_ERROR;
-    std::call_once(once, [] { init = hsa_init(); });  // reference-counted; the HIP runtime holds one too
-    if (init != HSA_STATUS_SUCCESS) return fail("of3d: hsa_init failed");
-    hsa_signal_t sig;
-    if (hsa_signal_create(n, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) return fail("of3d: hsa_signal_create failed");
-    int issued = 0;
-    std::string err;
-    for (; issued < n; ++issued) {
-        const int i = issued;
-        if (bytes[i] == 0) {
-            hsa_signal_subtract_relaxed(sig, 1);
-            continue;
-        }
-        hsa_amd_pointer_info_t si{}, di{};
-        si.size = sizeof(si);
-        di.size = sizeof(di);
-        if (hsa_amd_pointer_info(src[i], &si, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-            hsa_amd_pointer_info(dst[i], &di, nullptr, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
-            si.type == HSA_EXT_POINTER_TYPE_UNKNOWN || di.type == HSA_EXT_POINTER_TYPE_UNKNOWN) {
-            err = "of3d: dma copy needs device or pinned host buffers";
-            break;
-        }
-        if (hsa_amd_memory_async_copy(dst[i], di.agentOwner, src[i], si.agentOwner, bytes[i], 0, nullptr, sig) !=
-            HSA_STATUS_SUCCESS) {
-            err = "of3d: hsa_amd_memory_async_copy failed";
-            break;
-        }
-    }
-    if (issued < n) hsa_signal_subtract_relaxed(sig, n - issued);  // drop the copies never issued
-    hsa_signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED);
-    hsa_signal_destroy(sig);
-    if (!err.empty()) return fail(err.c_str());
-    return 0;
-}
-
-int of3d_flow_stats(const void* vx, const void* vy, const void* vz, const void* rel, int v_f32, int rel_f64,
-                    int64_t n, double thresh, double xyscale, double zscale, double tscale, double* out_vx,
-                    double* out_vy, double* out_vz, double* magnitude, double* theta, double* phi, void* stream) {
-    if (n < 0) return fail("of3d: negative element count");
-    if (n == 0) return 0;
-    if (!vx || !vy || !rel || !out_vx || !out_vy || !magnitude || !theta) return fail("of3d: null argument");
-    if (vz && (!out_vz || !phi)) return fail("of3d: null argument");
-    hipStream_t s = (hipStream_t)stream;
-    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 32);
-    auto launch = [&](auto vt, auto rt) {
-        using VT = decltype(vt);
-        using RT = decltype(rt);
-        hipLaunchKernelGGL((k_flow_stats<VT, RT>), dim3(blocks), dim3(256), 0, s, (const VT*)vx, (const VT*)vy,
-                           (const VT*)vz, (const RT*)rel, (size_t)n, thresh, xyscale, zscale, tscale, out_vx, out_vy,
-                           out_vz, magnitude, theta, phi);
-    };
-    if (v_f32)
-        rel_f64 ? launch(float{}, double{}) : launch(float{}, float{});
-    else
-        rel_f64 ? launch(double{}, double{}) : launch(double{}, float{});
-    OF3D_HIP(hipGetLastError());
-    return 0;
-}
-
-int of3d_copy_async(void* dst, const void* src, size_t bytes, int max_blocks, void* stream) {
-    if (bytes == 0) return 0;
-    if (!dst || !src) return fail("of3d: null argument");
-    if (max_blocks < 0) return fail("of3d: max_blocks must be >= 0");
-    const unsigned mb = max_blocks ? (unsigned)max_blocks : 64u;
-    hipStream_t s = (hipStream_t)stream;
-    if ((uintptr_t)dst % 16 == 0 && (uintptr_t)src % 16 == 0) {
-        const size_t n16 = bytes / 16;
-        const int tail = (int)(bytes % 16);
-        const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(mb, (n16 + 255) / 256));
-        hipLaunchKernelGGL(k_copy, dim3(blocks), dim3(256), 0, s, (const u32x4*)src, (u32x4*)dst, n16,
-                           (const unsigned char*)src + n16 * 16, (unsigned char*)dst + n16 * 16, tail);
-    } else {
-        const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(mb, (bytes + 255) / 256));
-        hipLaunchKernelGGL(k_copy_bytes, dim3(blocks), dim3(256), 0, s, (const unsigned char*)src,
-                           (unsigned char*)dst, bytes);
-    }
-    OF3D_HIP(hipGetLastError());
-    return 0;
-}
-
-}  // extern "C"
