@@ -275,7 +275,8 @@ def timed_region(step, plan, args, world, dev):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if plan is not None:
-        dom_ms = fused_names(plan.stage_times())[dom]
+        t = plan.stage_times()
+        dom_ms = t["prod_wy" if dom == "prod_wy_wx" else dom]
     return elapsed, profile, dom, dom_ms
 
 
@@ -391,6 +392,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="c3 = configs[2], the largest single-GPU config (the headline); c2 = configs[1]")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap", type=int, default=int(os.environ.get("OF3D_BENCH_OVERLAP", "-1")),
+                    help="z chunk (output planes) of the plan's overlap mode; 0 = serial; -1 = the plan's default")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
                     help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
@@ -439,6 +442,8 @@ def main():
 
     plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=dev.index, timing=max(args.steps, 1),
                      mode=_lib.OF3D_FP32 if fp32 else 0)
+    if args.overlap >= 0:
+        plan.set_overlap(args.overlap)
     fptrs = [d_in[i].data_ptr() for i in range(nwin)]
     stream = torch.cuda.current_stream(dev).cuda_stream
 

@@ -152,6 +152,16 @@ int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, i
 int of3d_plan_set_timing(of3d_plan* plan, int slots);
 int of3d_plan_set_timing_mask(of3d_plan* plan, unsigned mask);
 int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
+
+/* Overlap mode (3D plans with the fused products/W-xy kernel): of3d_plan_execute
+ * splits the output planes into chunks of `chunk_planes` (<= 0: off, the default
+ * unless OF3D_ZCHUNK is set; at most 16 chunks) and runs the HBM-bound gradient
+ * stages of chunk c+1 on the caller's stream beside the VALU-bound W-xy / W-z /
+ * solve stages of chunk c on the plan's second stream (joined back into the
+ * caller's stream before the call's work completes).  Results are bit-identical
+ * to the serial order.  A per-stage profile (timing mask with several stages)
+ * runs serially; with one timed stage its time is summed over the chunks. */
+int of3d_plan_set_overlap(of3d_plan* plan, int64_t chunk_planes);
 const char* of3d_stage_name(int i);
 
 /* Copy `bytes` from src to dst on `stream` with a kernel of at most

@@ -37,6 +37,7 @@ EXPORTED = (
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
+    "of3d_plan_set_overlap",
 )
 
 
@@ -113,6 +114,8 @@ def load():
         lib.of3d_plan_set_timing.restype = ctypes.c_int
         lib.of3d_plan_set_timing_mask.argtypes = [P, ctypes.c_uint]
         lib.of3d_plan_set_timing_mask.restype = ctypes.c_int
+        lib.of3d_plan_set_overlap.argtypes = [P, i64]
+        lib.of3d_plan_set_overlap.restype = ctypes.c_int
         d = ctypes.c_double
         lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
         lib.of3d_flow_stats.restype = ctypes.c_int
@@ -202,6 +205,11 @@ class Plan:
         return {self.lib.of3d_stage_name(i).decode(): buf[i] for i in range(n) if buf[i] >= 0}
 
     STAGES = ("grad_xy", "grad_z", "prod_wy", "wx", "wz_solve")
+
+    def set_overlap(self, chunk_planes):
+        """of3d_plan_set_overlap: z chunks of chunk_planes output planes, gradient stages of the next
+        chunk beside the W-xy / W-z / solve stages of this one (0: serial)."""
+        check(self.lib.of3d_plan_set_overlap(self.handle, int(chunk_planes)))
 
     def set_timing_stages(self, names=None):
         """Time only these stages (None: all); fewer events, less perturbation."""

@@ -15,11 +15,38 @@ const void* k34_fn(int rw, int s, int rb) {
     switch (rw) {
         OF3D_K34(12, 16, 8)
         OF3D_K34(15, 16, 8)
-        OF3D_K34(21, 8, 4)  // register ring of 44-48 rows: shorter tiles
+    case 21:  // register ring of 44-48 rows: shorter tiles
+        if (s == 8) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, 21, 8>;
+        if (s == 4) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, 21, 4>;
+        return nullptr;
         default: return nullptr;
     }
 #undef OF3D_K34
 }
+
+// Unique-staging instances (k_prod_wyx UQ: no duplicated halo columns, edge replicas copied)
+// for 8-wave blocks, cut for 2 waves per SIMD (256 VGPRs: an 8-wave block runs one per CU
+// anyway): gradient prefetch 4 rows, phase-B LDS distance 2.  c3 (rw 21): 8-row tiles
+// 1.85 ms vs 1.92 (4-row) and 2.02 (duplicate staging, 4-wave blocks); 16-row tiles and
+// deeper prefetch (8, 11 rows) or LDS distance 4 within noise.
+template <typename F, int NP>
+const void* k34_fn_uq(int rw, int s) {
+#define OF3D_K34U(RW)                                                                      \
+    if (rw == RW) {                                                                        \
+        if (s == 8) return (const void*)k_prod_wyx<F, NP, RW, 8, 4, 2, 4, 2, true>;        \
+        if (s == 4) return (const void*)k_prod_wyx<F, NP, RW, 4, 4, 2, 4, 2, true>;        \
+    }
+    OF3D_K34U(21)
+    OF3D_K34U(15)
+    OF3D_K34U(12)
+#undef OF3D_K34U
+    return nullptr;
+}
+
+template const void* k34_fn_uq<double, 9>(int, int);
+template const void* k34_fn_uq<double, 5>(int, int);
+template const void* k34_fn_uq<float, 9>(int, int);
+template const void* k34_fn_uq<float, 5>(int, int);
 
 template const void* k34_fn<double, 9>(int, int, int);
 template const void* k34_fn<double, 5>(int, int, int);

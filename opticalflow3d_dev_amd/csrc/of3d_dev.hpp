@@ -656,6 +656,21 @@ constexpr int k34_nr(int rw, int s) { return ((2 * rw + 2 + s - 1) / s) * s; }
 // r mod 4 (mod 32) elements (bank-conflict-free phase B, see k_prod_wyx)
 __host__ __device__ constexpr int k34_row(int r, int cwp) { return r * cwp + 28 * (r / 4); }
 __host__ __device__ constexpr int k34_tile(int s, int cwp) { return s * cwp + 28 * (s / 4); }  // per tile buffer
+// tile row pitch for a block of tx outputs: its 2 rw halo positions, = 1 (mod 32)
+__host__ __device__ constexpr int k34_pitch(int tx, int rw) { return ((tx + 2 * rw + 31) & ~31) + 1; }
+
+// value of lane `lane` (wave-uniform index) of a per-lane F, to every lane of the wave
+template <typename F>
+__device__ __forceinline__ F bcast_lane(F v, int lane) {
+    if constexpr (sizeof(F) == 8) {
+        const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, lane);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), lane);
+        return __builtin_bit_cast(F, ((unsigned long long)hi << 32) | lo);
+    } else {
+        return __builtin_bit_cast(F, __builtin_amdgcn_readlane(__builtin_bit_cast(unsigned, v), lane));
+    }
+}
 
 __device__ __forceinline__ void lds_barrier() {
     // LDS-only barrier: global loads in flight stay in flight (__syncthreads
@@ -707,14 +722,17 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
     }
 }
 
-template <typename F, int NP, int RW, int S, int RB = 4>
-__global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
-                                                                 int nx, size_t fs, const F* __restrict__ hw,
-                                                                 int tx, int nyc, int nbx, int nyb, int cpg,
-                                                                 int ngroups) {
+// OCC: waves per SIMD the register budget is cut for (3: 168 VGPRs; 2: 256, for 8-wave blocks,
+// which run one per CU anyway); PDX: gradient prefetch rows (0: as far as OCC 3 allows);
+// DB: LDS prefetch distance of the phase-B pass; UQ: staging (below).
+template <typename F, int NP, int RW, int S, int RB = 4, int OCC = OF3D_K34_OCC, int PDX = 0, int DB = 2,
+          bool UQ = false>
+__global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
+                                                       int nx, size_t fs, const F* __restrict__ hw, int tx,
+                                                       int nyc, int nbx, int nyb, int cpg, int ngroups) {
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
-    constexpr int PD0 = sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8);
+    constexpr int PD0 = PDX ? PDX : (sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8));
 #ifdef OF3D_K34_PD
     constexpr int PD = NR % OF3D_K34_PD == 0 ? OF3D_K34_PD : PD0;  // experiments
 #else
@@ -725,7 +743,7 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
     static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* sw = reinterpret_cast<F*>(smem_raw);  // two W-y tiles [2][S][cwp] (tile n in buffer n & 1)
-    const int cw = blockDim.x, cwp = cw + 1;
+    const int cwp = UQ ? k34_pitch(min(tx, nx), RW) : (int)blockDim.x + 1;
     const int t = threadIdx.x;
     // XCD-aware block decode: group g = (plane, run of cpg row chunks), member m = (chunk in the
     // run, product, column block): one group's blocks share an XCD and are dispatched together
@@ -743,11 +761,49 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
     const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
     const int xo0 = bx * tx;
     const int txu = min(tx, nx - xo0);  // useful outputs of this block
-    // waves with no staged column (the last column block of a row is often narrow)
-    // leave at once; barriers count only the waves still running
-    const int wa = (min(cw, txu + 2 * RW) + 63) >> 6, ca = 64 * wa;
+    // Staged columns, tile position i <-> column xo0 - RW + i.
+    // UQ = false: thread t stages column clamp(xo0 - RW + t) at position t, halo positions
+    //   outside the volume (mode='nearest') recomputed as duplicates of the edge column
+    //   (txu + 2 RW <= blockDim.x by the host's geometry).
+    // UQ = true: the block's outputs and their W-x halo inside the volume, each once
+    //   ([sxs, sxs + ns), ns <= blockDim.x): thread t holds column sxs + t at position padL + t;
+    //   the positions outside the volume are edge replicas copied once per tile (no halo work
+    //   at all for a block covering the whole row).
+    const int sxs = UQ ? max(xo0 - RW, 0) : xo0 - RW;
+    const int ns = UQ ? min(xo0 + txu + RW, nx) - sxs : txu + 2 * RW;
+    const int padL = UQ ? sxs - (xo0 - RW) : 0, padR = UQ ? (xo0 + txu + RW) - (sxs + ns) : 0;
+    // waves with no staged column leave at once; barriers count only the waves still running
+    const int wa = (ns + 63) >> 6, ca = 64 * wa;
     if (t >= ca) return;
-    const unsigned vof = (unsigned)clampi(xo0 - RW + t, 0, nx - 1) * ES;  // staged column of this thread
+    const unsigned vof = (unsigned)clampi(sxs + t, 0, nx - 1) * ES;  // staged column of this thread
+    // wave index in an SGPR: the edge-replica branches below are scalar, not exec-masked
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+    const bool lpad = UQ && padL > 0 && wv == 0;                  // wave 0 holds column 0 in lane 0
+    const bool rpad = UQ && padR > 0 && wv == ((ns - 1) >> 6);    // this wave holds column nx - 1
+    // UQ: lanes past ns (last wave) compute a duplicate and store it past the row's positions
+    // (pitch cwp >= txu + 2 RW + 1; that slot only feeds outputs >= txu, never stored)
+    const int wpos = !UQ ? t : (t < ns ? padL + t : padL + ns + padR);
+    // W-y result of one row into the tile; the edge replicas are copied once per tile by the
+    // wave that wrote the edge column (its own LDS writes are ordered before its reads)
+    auto put = [&](F* row, F a) { row[wpos] = a; };
+    auto replicas = [&](F* tile) {
+        if (lpad) {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                F* row = tile + k34_row(r, cwp);
+                const F e = row[padL];
+                if (ln < padL) row[ln] = e;
+            }
+        }
+        if (rpad) {
+#pragma unroll
+            for (int r = 0; r < S; ++r) {
+                F* row = tile + k34_row(r, cwp);
+                const F e = row[padL + ns - 1];
+                if (ln < padR) row[padL + ns + ln] = e;
+            }
+        }
+    };
     constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;  // as k_prod_wy
     constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
     const size_t pl = (size_t)zl * ny * nx;
@@ -792,7 +848,7 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
             const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
             if (sg >= nseg) continue;
             F out[RB];
-            lds_pass_c<RB, RW, 2>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
+            lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
             if (r < nr) {
                 // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
                 const int c0 = RB * sg;
@@ -844,12 +900,13 @@ __global__ __launch_bounds__(512, OF3D_K34_OCC) void k_prod_wyx(const F* __restr
 #else
                                 ring[ic1 % NR] = p1;
 #endif
-                                tile[k34_row(j % S, cwp) + t] = a0;
-                                tile[k34_row((j + 1) % S, cwp) + t] = a1;
+                                put(tile + k34_row(j % S, cwp), a0);
+                                put(tile + k34_row((j + 1) % S, cwp), a1);
                             }(),
                             ...);
                     }(std::make_integer_sequence<int, S / 2>{});
                     const int yb = u0 + h0;
+                    if constexpr (UQ) replicas(tile);
                     phase_b(tile, y0 + yb, min(S, nrows - yb));
                     if (yb + S >= nrows) done = true;
                 }(),

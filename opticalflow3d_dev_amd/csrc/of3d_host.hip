@@ -36,6 +36,7 @@ int symmetry(const double* w, int r) {
 
 const char* kStageNames[] = {"grad_xy", "grad_z", "prod_wy", "wx", "wz_solve"};
 constexpr int kStages = 5;
+constexpr int kMaxChunks = 16;  // overlap mode: most z chunks per execution
 
 }  // namespace
 
@@ -72,7 +73,14 @@ struct of3d_plan {
     std::vector<K34Geom> k34_cand;  // geometries that keep >= 8 waves per CU (k34_tune picks)
     bool host_ev = false;            // host entry: record into ev[]
     hipEvent_t ev[kStages + 1] = {};
+    // overlap mode (run_t): output planes per chunk (0 = serial), second stream, chunk events
+    int64_t zchunk = 0;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_chunk[kMaxChunks] = {};
     int timing_slots = 0;            // of3d_plan_set_timing: ring of per-execution event sets
+    int tev_per_slot = kStages + 1;  // events per slot: serial boundaries or 2 per chunk of one stage
+    std::vector<int> tchunks;        // per slot: chunks timed (overlap mode, one stage) or 0 (serial)
     unsigned timing_mask = (1u << kStages) - 1;  // stages timed (events at their two boundaries)
     std::vector<hipEvent_t> tev;     // timing_slots * (kStages + 1)
     int64_t tcount = 0;              // executions recorded since the last of3d_plan_stage_times
@@ -163,10 +171,29 @@ int k0_vec_width(int dtype) {
 
 
 
-// K34 geometry: waves per block nw in {1, 2, 4} (staged columns cw = 64 nw,
-// tx = (cw - 2rw) & ~3 outputs) and tile rows S.  Fewest staged lanes over the
-// row (halo + idle lanes) among the shapes that keep >= 8 waves per CU resident
-// (LDS and registers from the occupancy API), ties to the higher occupancy.
+// K34 geometry.  Two kernel families:
+//  - duplicate staging (k_prod_wyx UQ = false, 168 VGPRs): blocks of nw in {1, 2, 3, 4} waves,
+//    cw = 64 nw staged columns, tx = (cw - 2 rw) & ~3 outputs (halo columns recomputed,
+//    clamped ones as duplicates of the edge column);
+//  - unique staging (UQ = true, 256 VGPRs, nw in {4, 8}): each column once, edge replicas
+//    copied, so a block covering the whole row (nx <= 64 nw) stages no halo at all; the column
+//    stride is the one with the fewest staged lanes.
+// The heuristic pick: fewest staged lanes among the duplicate-staging shapes keeping >= 8 waves
+// per CU resident (LDS and registers from the occupancy API), ties to the higher occupancy;
+// k34_tune then times every candidate of both families on the plan's workspace.
+// Staged lanes of the stride-tx unique-staging partition of a row, and the widest block.
+long k34_lanes(int nx, int rw, int tx, int& widest) {
+    long lanes = 0;
+    widest = 0;
+    for (int x0 = 0; x0 < nx; x0 += tx) {
+        const int txu = std::min(tx, nx - x0);
+        const int ns = std::min(x0 + txu + rw, nx) - std::max(x0 - rw, 0);
+        widest = std::max(widest, ns);
+        lanes += 64L * ((ns + 63) / 64);
+    }
+    return lanes;
+}
+
 template <typename F>
 int k34_setup(of3d_plan* p, int np) {
     p->k34 = {};
@@ -179,48 +206,68 @@ int k34_setup(of3d_plan* p, int np) {
     int best_waves = 0;
     const char* env_nw = getenv("OF3D_K34_NW");  // overrides (experiments)
     const char* env_s = getenv("OF3D_K34_S");
+    const char* env_uq = getenv("OF3D_K34_UQ");  // 0: duplicate staging only, 1: unique only
+    auto occupancy = [&](const void* fn, int cw, size_t lds, int& waves) -> int {
+        OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        int nb = 0;
+        OF3D_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, cw, lds));
+        waves = nb * (cw / 64);
+        return 0;
+    };
     for (int s : {16, 8, 4}) {
         if (env_s && atoi(env_s) != s) continue;
-      for (int rb : {4, 2}) {
-        if (getenv("OF3D_K34_RB") && atoi(getenv("OF3D_K34_RB")) != rb) continue;
-        const void* fn = np == 9 ? k34_fn<F, 9>(rw, s, rb) : k34_fn<F, 5>(rw, s, rb);
-        if (!fn) continue;
+        const void* fd = (env_uq && env_uq[0] == '1') ? nullptr
+                                                       : (np == 9 ? k34_fn<F, 9>(rw, s, 4) : k34_fn<F, 5>(rw, s, 4));
+        const void* fu = (env_uq && env_uq[0] == '0') ? nullptr : (np == 9 ? k34_fn_uq<F, 9>(rw, s) : k34_fn_uq<F, 5>(rw, s));
         for (int nw : {1, 2, 3, 4, 8}) {  // launch bound 512
-            // blocks of 5-7 waves measured as if one block per CU fitted (c2: nw 5, 6, 7 all
-            // ~300 us vs 242 us at nw 2); keep whole-SIMD multiples
-            if (env_nw ? atoi(env_nw) != nw : nw == 8) continue;
-            const int cw = 64 * nw, tx = (cw - 2 * rw) & ~3;  // tx: whole phase-B items
-            if (tx < 8) continue;
-            const int nbx = (nx + tx - 1) / tx;
-            const size_t lds = (size_t)2 * k34_tile(s, cw + 1) * es;  // two W-y tiles
-            if (lds > 160 * 1024) continue;
-            OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            int nb = 0;
-            OF3D_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, cw, lds));
-            const int waves = nb * nw;
-            if (waves == 0) continue;
-            const long lanes = (long)(nbx - 1) * cw + 64 * ((nx - (nbx - 1) * tx + 2 * rw + 63) / 64);
-            const bool ok = waves >= 8, best_ok = best_waves >= 8;
-            if (ok) {
-                OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-                p->k34_cand.push_back({fn, cw, s, tx, nbx, lds});
+            if (env_nw && atoi(env_nw) != nw) continue;
+            const int cw = 64 * nw;
+            if (fd && nw <= 4) {  // duplicate staging
+                const int tx = (cw - 2 * rw) & ~3;  // whole phase-B items
+                if (tx >= 8) {
+                    const int nbx = (nx + tx - 1) / tx;
+                    const size_t lds = (size_t)2 * k34_tile(s, cw + 1) * es;  // two W-y tiles
+                    int waves = 0;
+                    if (lds <= 160 * 1024 && !occupancy(fd, cw, lds, waves) && waves > 0) {
+                        const long lanes = (long)(nbx - 1) * cw + 64 * ((nx - (nbx - 1) * tx + 2 * rw + 63) / 64);
+                        const bool ok = waves >= 8, best_ok = best_waves >= 8;
+                        if (ok) p->k34_cand.push_back({fd, cw, s, tx, nbx, lds});
+                        const bool better =
+                            !p->k34.fn || (ok && !best_ok) ||
+                            (ok == best_ok &&
+                             (ok ? (lanes < best_lanes || (lanes == best_lanes && waves > best_waves)) : waves > best_waves));
+                        if (better) {
+                            p->k34 = {fd, cw, s, tx, nbx, lds};
+                            best_lanes = lanes;
+                            best_waves = waves;
+                        }
+                    }
+                }
             }
-            const bool better = !p->k34.fn || (ok && !best_ok) ||
-                                (ok == best_ok && (ok ? (lanes < best_lanes || (lanes == best_lanes && waves > best_waves))
-                                                      : waves > best_waves));
-            if (better) {
-                p->k34.fn = fn;
-                p->k34.cw = cw;
-                p->k34.s = s;
-                p->k34.tx = tx;
-                p->k34.nbx = nbx;
-                p->k34.lds = lds;
-                best_lanes = lanes;
-                best_waves = waves;
+            if (fu && nw >= 4) {  // unique staging: the column stride with the fewest staged lanes
+                int tx = 0;
+                long lanes = 0;
+                for (int nbx = 1; nbx <= 64; ++nbx) {
+                    const int t = nbx == 1 ? nx : ((nx + nbx - 1) / nbx + 3) & ~3;
+                    if (t < 8) break;
+                    int widest = 0;
+                    const long l = k34_lanes(nx, rw, t, widest);
+                    if (widest > cw) continue;
+                    if (!tx || l < lanes) tx = t, lanes = l;  // ties: the wider stride, fewer blocks
+                }
+                if (tx) {
+                    const int nbx = (nx + tx - 1) / tx;
+                    const size_t lds = (size_t)2 * k34_tile(s, k34_pitch(std::min(tx, nx), rw)) * es;
+                    int waves = 0;
+                    if (lds <= 160 * 1024 && !occupancy(fu, cw, lds, waves) && waves >= nw)
+                        p->k34_cand.push_back({fu, cw, s, tx, nbx, lds});
+                }
             }
         }
-      }
     }
+    if (!p->k34.fn && !p->k34_cand.empty()) p->k34 = p->k34_cand.front();
+    for (const auto& k : p->k34_cand)
+        OF3D_HIP(hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (p->k34.fn)
         OF3D_HIP(hipFuncSetAttribute(p->k34.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (getenv("OF3D_VERBOSE") && p->k34.fn)
@@ -296,12 +343,16 @@ int k34_tune(of3d_plan* p) {
     for (size_t i = 0; i < p->k34_cand.size(); ++i) {
         const auto& k = p->k34_cand[i];
         OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));  // warm
-        OF3D_HIP(hipEventRecord(e0, p->stream));
-        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
-        OF3D_HIP(hipEventRecord(e1, p->stream));
-        OF3D_HIP(hipEventSynchronize(e1));
-        float ms = 0.f;
-        OF3D_HIP(hipEventElapsedTime(&ms, e0, e1));
+        float ms = 1e30f;
+        for (int rep = 0; rep < 2; ++rep) {  // best of two
+            OF3D_HIP(hipEventRecord(e0, p->stream));
+            OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+            OF3D_HIP(hipEventRecord(e1, p->stream));
+            OF3D_HIP(hipEventSynchronize(e1));
+            float m = 0.f;
+            OF3D_HIP(hipEventElapsedTime(&m, e0, e1));
+            ms = std::min(ms, m);
+        }
         if (i == 0 ? true : ms < 0.97f * best) best = ms, bi = i;
     }
     (void)hipEventDestroy(e0);
@@ -375,21 +426,35 @@ Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
     return r;
 }
 
+// The stage pipeline over output planes [zo0, zo1).  Stage launches take plane sub-ranges:
+//   K0 + K1 : pre-z fields B on planes [b0, b1)      (input frames, D0 temporary)
+//   K2      : gradients G on planes [q0, q1)         (reads B on [q0 - rd, q1 + rd))
+//   K34     : W-xy of the products, Q on [q0, q1)     (per plane)
+//   K5      : outputs on [o0, o1)                     (reads Q on [o0 - rw, o1 + rw))
+// Workspace (3D): Y0 = D0, Y4..7 = B, Y0..3 = G, X0..8 = Q; plane origins zb0 (D0, B) and
+// zg0 (G, Q).  Serial mode: one chunk on the caller's stream.  Overlap mode (fused K34,
+// p->zchunk > 0): the output range in chunks of zchunk planes, K0-K2 of every chunk on the
+// caller's stream and K34 + K5 on the plan's second stream, each chunk's K34 behind an
+// event after its K2 — the HBM-bound K0-K2 of chunk c+1 run beside the VALU-bound K34/K5
+// of chunk c.  Every plane range is disjoint from the ones the other stream touches at the
+// same time (B/G/D0 planes of later chunks lie above the G/Q planes of earlier ones), and
+// the results are those of the serial order (same kernels, same planes, global clamping).
 template <typename F>
 int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx_,
           void* vy_, void* vz_, void* rel, hipStream_t s) {
+    if (!p) return fail("of3d: null plan");
     F* vx = (F*)vx_;
     F* vy = (F*)vy_;
     F* vz = (F*)vz_;
     F* X = (F*)p->X;
     F* Y = (F*)p->Y;
-    if (!p) return fail("of3d: null plan");
     if (zo0 < 0 || zo1 > p->nz || zo0 >= zo1) return fail("of3d: bad output plane range");
     const Ranges R = ranges(p, zo0, zo1);
     if (R.zb1 - R.zb0 > p->cap_planes) return fail("of3d: output range exceeds the plan's workspace");
     if (frame_z0 > R.zb0) return fail("of3d: frames do not hold the stencil halo planes");
     if (dtype_size(dtype) == 0) return fail("of3d: unsupported dtype");
     const int ny = (int)p->ny, nx = (int)p->nx;
+    const bool d3 = p->ndim == 3;
     Frames fr{};
     for (int i = 0; i < 2 * p->rt + 1; ++i) {
         if (!d_frames[i]) return fail("of3d: null frame pointer");
@@ -397,32 +462,31 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     }
     const DevTaps<F> tp = dev_taps<F>(p);
     const size_t fs = p->fs;
-    const int nb = (int)(R.zb1 - R.zb0), ng = (int)(R.zg1 - R.zg0), no = (int)(R.zo1 - R.zo0);
-    hipEvent_t* evs = p->host_ev ? p->ev
-                      : (p->timing_slots ? &p->tev[(size_t)(p->tcount % p->timing_slots) * (kStages + 1)] : nullptr);
-    // boundary i opens stage i and closes stage i-1; untimed stages get no events
-    // (every event is a barrier packet between kernels: a few microseconds each)
-    const unsigned bmask = p->host_ev ? ~0u : (p->timing_mask | (p->timing_mask << 1));
-#define OF3D_MARK(i) \
-    do { \
-        if (evs && ((bmask >> (i)) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s)); \
-    } while (0)
-    OF3D_MARK(0);
-    // K0 + K1 — frames equally spaced (one stack) are addressed by stride
-    {
-        const size_t es = dtype_size(dtype);
+    const size_t plane = (size_t)ny * nx;
+    const size_t es = dtype_size(dtype);
+    const int nwin = 2 * p->rt + 1;
+    const int nf = d3 ? 9 : 5;
+    // field buffers
+    F* D0b = Y;                        // temporal derivative (K0 -> K1), origin zb0
+    F* Bb = d3 ? Y + 4 * fs : X;       // pre-z fields (3D) / final gradients (2D), origin zb0
+    const F* Gb = d3 ? Y : X;          // gradients, origin zg0
+    F* Pb = d3 ? X : Y;                // K3 W-y (fallback) / K34 W-xy
+    F* Qb = p->k34.fn ? Pb : (d3 ? Y : X);  // W-xy (K4 fallback writes the other buffer)
+
+    // ---- stage launches over plane sub-ranges ----
+    auto k01 = [&](int64_t b0, int64_t b1, hipStream_t st) -> int {
+        if (b1 <= b0) return 0;
+        const int nb = (int)(b1 - b0);
         long long fstride = 0;
-        const int nwin = 2 * p->rt + 1;
         if (nwin > 1) {
             const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
             bool eq = d > 0 && d % (long long)es == 0;
             for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
             if (eq) fstride = d / (long long)es;
         }
-        const size_t plane = (size_t)ny * nx;
-        size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)nb * plane;
+        size_t off0 = (size_t)(b0 - frame_z0) * plane, n = (size_t)nb * plane;
         int rt_arg = p->rt;
-        F* D0 = Y;  // Y field 0 is free until K2 writes it
+        F* D0 = D0b + (size_t)(b0 - R.zb0) * plane;
         const int V = k0_vec_width(dtype);
         const size_t vb = (size_t)V * es;
         bool vec = off0 % V == 0 && n % V == 0;
@@ -434,137 +498,212 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             const void* k0 = k0c_fn<F>(dtype, p->rt);
             if (k0) {
                 void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
-                OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, s));
+                OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, st));
             } else {
-                OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
+                OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
             }
         } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
             void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
                             (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, s));
+            OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
         }
-        {
-            const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
-            const F* D0c = D0;
-            int need_b4 = p->ndim == 3, nb_arg = nb;
-            dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
-            void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
-                            (void*)&X, (void*)&fs, (void*)&need_b4};
-            // (32-bit buffer offsets within a plane: planes up to 2 GiB)
-            const bool k1c_ok = p->k1c && (size_t)ny * nx * sizeof(F) <= 0x7fffffffu;
-            const void* k1c = k1c_ok ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
-            if (k1c) {
-                // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
-                static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
-                static const int nyc_env = getenv("OF3D_K1C_NYC") ? atoi(getenv("OF3D_K1C_NYC")) : 32;
-                const int cw = cw_env ? cw_env : (nx <= 256 ? 128 : 256);  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
-                int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
-                int nyc = std::min(ny, nyc_env), nyb;
-                while (true) {
-                    nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
-                    nyb = (ny + nyc - 1) / nyc;
-                    if ((long)nb * nyb * nbx <= 8192 || nyc >= ny) break;
-                    nyc *= 2;
-                }
-                const size_t lds = (size_t)6 * k34_tile(K1C_S, cw + 1) * sizeof(F);
-                const unsigned blocks = (unsigned)((long)nb * nyb * nbx);
-                void* cargs[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&tp, (void*)&X,
-                                 (void*)&fs, (void*)&need_b4, (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb};
-                OF3D_HIP(hipLaunchKernel(k1c, dim3(blocks), dim3(cw), cargs, lds, s));
-            } else {
-                OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, s));
+        const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
+        const F* D0c = D0;
+        F* Bo = Bb + (size_t)(b0 - R.zb0) * plane;
+        int need_b4 = d3, nb_arg = nb;
+        dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
+        void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
+                        (void*)&Bo, (void*)&fs, (void*)&need_b4};
+        // (32-bit buffer offsets within a plane: planes up to 2 GiB)
+        const bool k1c_ok = p->k1c && plane * sizeof(F) <= 0x7fffffffu;
+        const void* k1c = k1c_ok ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
+        if (k1c) {
+            // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
+            static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
+            static const int nyc_env = getenv("OF3D_K1C_NYC") ? atoi(getenv("OF3D_K1C_NYC")) : 32;
+            const int cw = cw_env ? cw_env : (nx <= 256 ? 128 : 256);  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
+            int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
+            int nyc = std::min(ny, nyc_env), nyb;
+            while (true) {
+                nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
+                nyb = (ny + nyc - 1) / nyc;
+                if ((long)nb * nyb * nbx <= 8192 || nyc >= ny) break;
+                nyc *= 2;
             }
+            const size_t lds = (size_t)6 * k34_tile(K1C_S, cw + 1) * sizeof(F);
+            const unsigned blocks = (unsigned)((long)nb * nyb * nbx);
+            void* cargs[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&tp, (void*)&Bo,
+                             (void*)&fs, (void*)&need_b4, (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb};
+            OF3D_HIP(hipLaunchKernel(k1c, dim3(blocks), dim3(cw), cargs, lds, st));
+        } else {
+            OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, st));
         }
-    }
-    OF3D_MARK(1);
-    const F* G;
-    if (p->ndim == 3) {
+        return 0;
+    };
+    auto k2 = [&](int64_t q0, int64_t q1, hipStream_t st) -> int {
+        if (q1 <= q0 || !d3) return 0;
+        const int ng = (int)(q1 - q0);
         const void* k2c = nullptr;
         if (p->k2c) {
             if (p->rd == 6 && p->rs == 2) k2c = (const void*)k_grad_z_c<F, 6, 2>;
             if (p->rd == 3 && p->rs == 1) k2c = (const void*)k_grad_z_c<F, 3, 1>;
         }
+        const F* Bc = Bb;
+        F* Go = Y + (size_t)(q0 - R.zg0) * plane;
+        // input planes clamp at zb1 (= nz at the top edge): see the K5 launch
+        int zb0 = (int)R.zb0, zg0 = (int)q0, ngz = ng, nzz = (int)R.zb1;
         if (k2c) {
             // z march: 256 columns per block, chunks of >= 32 planes (2 rd halo planes re-read per chunk)
-            const int plane = ny * nx;
+            const int pl = (int)plane;
             int zc = std::min(ng, 32);
-            while ((long)cdiv(plane, 256) * cdiv(ng, zc) > 8192 && zc < ng) zc *= 2;
-            const F* Bc = X;
-            // input planes clamp at zb1 (= nz at the top edge): see the K5 launch
-            int zb0 = (int)R.zb0, zg0 = (int)R.zg0, ngz = ng, nzz = (int)R.zb1;
-            void* args[] = {(void*)&Bc, (void*)&zb0, (void*)&Y, (void*)&zg0, (void*)&ngz, (void*)&nzz, (void*)&plane,
+            while ((long)cdiv(pl, 256) * cdiv(ng, zc) > 8192 && zc < ng) zc *= 2;
+            void* args[] = {(void*)&Bc, (void*)&zb0, (void*)&Go, (void*)&zg0, (void*)&ngz, (void*)&nzz, (void*)&pl,
                             (void*)&fs, (void*)&tp, (void*)&zc};
-            OF3D_HIP(hipLaunchKernel(k2c, dim3(cdiv(plane, 256), cdiv(ng, zc)), dim3(256), args, 0, s));
+            OF3D_HIP(hipLaunchKernel(k2c, dim3(cdiv(pl, 256), cdiv(ng, zc)), dim3(256), args, 0, st));
         } else {
             dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
-            hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, s, X, (int)R.zb0, Y, (int)R.zg0, ng,
-                               (int)R.zb1, ny, nx, fs, tp);
+            hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, st, Bc, zb0, Go, zg0, ngz, nzz, ny, nx, fs, tp);
             OF3D_HIP(hipGetLastError());
         }
-        G = Y;
-    } else {
-        G = X;
-    }
-    OF3D_MARK(2);
-    F* P = p->ndim == 3 ? X : Y;
-    F* Q = p->ndim == 3 ? Y : X;  // W-xy result (K4), or P when K34 writes it (G lives in Q's buffer)
-    if (p->k34.fn) Q = P;
-    const int nf = p->ndim == 3 ? 9 : 5;
-    if (p->k34.fn) {
-        // fused products + W y + W x (stage "prod_wy"; stage "wx" stays empty)
-        OF3D_HIP(launch_k34(p->k34, G, P, ng, nf, ny, nx, fs, tp.w, s));
-        OF3D_MARK(3);
-    } else {
-    {
-        dim3 g(cdiv(nx, 64), 1, ng * nf);
-        int rw_arg = p->rw;
-        void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
-                        (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, s));
-    }
-    OF3D_MARK(3);
-    {
+        return 0;
+    };
+    auto k34 = [&](int64_t q0, int64_t q1, hipStream_t st) -> int {
+        if (q1 <= q0) return 0;
+        const int ng = (int)(q1 - q0);
+        const size_t o = (size_t)(q0 - R.zg0) * plane;
+        OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st));
+        return 0;
+    };
+    auto k3k4 = [&](hipStream_t st) -> int {  // fallback: W y and W x as two kernels (whole range)
+        const int ng = (int)(R.zg1 - R.zg0);
+        F* P = Pb;
+        const F* G = Gb;
+        {
+            dim3 g(cdiv(nx, 64), 1, ng * nf);
+            int rw_arg = p->rw;
+            void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
+                            (void*)&rw_arg};
+            OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, st));
+        }
+        return 0;
+    };
+    auto k4 = [&](hipStream_t st) -> int {
+        const int ng = (int)(R.zg1 - R.zg0);
         dim3 g(1, cdiv(ny, K4_ROWS), ng * nf);
         int rw_arg = p->rw;
-        const F* Pc = P;
+        const F* Pc = Pb;
+        F* Q = Qb;
         void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
                         (void*)&rw_arg};
-        OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, s));
-    }
-    }
-    OF3D_MARK(4);
-    if (p->ndim == 3) {
-        const K5Geom kg = k5_geom(p->rw);
-        dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
-        int zg0 = (int)R.zg0, zo0 = (int)R.zo0, rw_arg = p->rw;
-        // window planes clamp at zg1 (= nz at the volume's top edge): the rows a block
-        // loads past its last output plane stay inside the workspace's W-xy planes
-        int zq1 = (int)R.zg1;
-        const F* Qc = Q;
-        void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                        (void*)&tp.wr, (void*)&rw_arg, (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-        if (p->k5c) {
-            dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
-            void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                             (void*)&zo0, (void*)&no, (void*)&vx, (void*)&vy, (void*)&vz, (void*)&rel};
-            OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, s));
-        } else if (p->k5_nb) {
-            const void* k5 = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
-            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5d_lds, s));
+        OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, st));
+        return 0;
+    };
+    auto k5 = [&](int64_t o0, int64_t o1, int64_t q1, hipStream_t st) -> int {
+        if (o1 <= o0) return 0;
+        const size_t oo = (size_t)(o0 - R.zo0) * plane;
+        F* ovx = vx + oo;
+        F* ovy = vy + oo;
+        F* ovz = d3 ? vz + oo : nullptr;
+        void* orel = (char*)rel + oo * (p->rel64 ? sizeof(double) : sizeof(float));  // 3D rel (2D: oo = 0)
+        if (d3) {
+            const K5Geom kg = k5_geom(p->rw);
+            const int no = (int)(o1 - o0);
+            dim3 g(cdiv(nx, 64), ny, cdiv(no, kg.g * kg.r));
+            int zg0 = (int)R.zg0, zoa = (int)o0, rw_arg = p->rw, noa = no;
+            // window planes clamp at q1 (= nz at the volume's top edge): the rows a block loads
+            // past its last output plane stay inside the W-xy planes computed so far
+            int zq1 = (int)q1;
+            const F* Qc = Qb;
+            void* args[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+                            (void*)&tp.wr, (void*)&rw_arg, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy,
+                            (void*)&ovz, (void*)&orel};
+            if (p->k5c) {
+                dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
+                void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
+                                 (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz, (void*)&orel};
+                OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, st));
+            } else if (p->k5_nb) {
+                const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
+                OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5d_lds, st));
+            } else {
+                const void* k = p->rel64 ? k5_kernel<F, double>(p->rw) : k5_kernel<F, float>(p->rw);
+                OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5_lds, st));
+            }
         } else {
-            const void* k5 = p->rel64 ? k5_kernel<F, double>(p->rw) : k5_kernel<F, float>(p->rw);
-            OF3D_HIP(hipLaunchKernel(k5, g, dim3(64, kg.g), args, p->k5_lds, s));
+            const int n = ny * nx;
+            hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st, (const F*)Qb, fs, n, vx, vy, (F*)rel);
+        }
+        OF3D_HIP(hipGetLastError());
+        return 0;
+    };
+
+    // ---- schedule ----
+    const int slot = p->timing_slots ? (int)(p->tcount % p->timing_slots) : 0;
+    hipEvent_t* evs = p->host_ev ? p->ev : (p->timing_slots ? &p->tev[(size_t)slot * p->tev_per_slot] : nullptr);
+    const unsigned tmask = p->host_ev ? (1u << kStages) - 1 : p->timing_mask;
+    const bool one_stage = evs && !p->host_ev && (tmask & (tmask - 1)) == 0;
+    // overlap only with the fused K34, and with no per-stage profile requested
+    const int64_t nout = R.zo1 - R.zo0;
+    int nch = 1;
+    if (d3 && p->k34.fn && p->zchunk > 0 && (!evs || one_stage)) {
+        nch = (int)std::min<int64_t>((nout + p->zchunk - 1) / p->zchunk, kMaxChunks);
+        if (nch < 2) nch = 1;
+    }
+    if (nch == 1) {
+        // serial: boundary i opens stage i and closes stage i-1; untimed stages get no events
+        // (every event is a barrier packet between kernels: a few microseconds each)
+        const unsigned bmask = tmask | (tmask << 1);
+        auto mark = [&](int i) -> int {
+            if (evs && ((bmask >> i) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s));
+            return 0;
+        };
+        if (mark(0) || k01(R.zb0, R.zb1, s) || mark(1) || k2(R.zg0, R.zg1, s) || mark(2)) return -1;
+        if (p->k34.fn) {
+            if (k34(R.zg0, R.zg1, s) || mark(3)) return -1;  // "prod_wy" holds W x too; "wx" stays empty
+        } else {
+            if (k3k4(s) || mark(3) || k4(s)) return -1;
+        }
+        if (mark(4) || k5(R.zo0, R.zo1, R.zg1, s) || mark(5)) return -1;
+        if (!p->host_ev && p->timing_slots) {
+            p->tchunks[slot] = 0;
+            ++p->tcount;
         }
     } else {
-        const int n = ny * nx;
-        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, s, Q, fs, n, vx, vy, (F*)rel);
+        // overlap: chunk c = outputs [o_c, o_c+1); its G/Q planes end rw above, its B planes rd above that
+        hipStream_t s2 = p->stream2;
+        OF3D_HIP(hipEventRecord(p->ev_fork, s));
+        OF3D_HIP(hipStreamWaitEvent(s2, p->ev_fork, 0));
+        const int tst = one_stage ? __builtin_ctz(tmask) : -1;  // the one timed stage (events per chunk)
+        int64_t b_prev = R.zb0, q_prev = R.zg0;
+        const int64_t cz = (nout + nch - 1) / nch;
+        for (int c = 0; c < nch; ++c) {
+            const int64_t o0 = R.zo0 + c * cz, o1 = std::min(o0 + cz, R.zo1);
+            const bool last = c == nch - 1;
+            const int64_t q1 = last ? R.zg1 : std::min(o1 + p->rw, R.zg1);
+            const int64_t b1 = last ? R.zb1 : std::min(q1 + p->rd, R.zb1);
+            auto tm = [&](int stage, int edge, hipStream_t st) -> int {
+                if (stage == tst) OF3D_HIP(hipEventRecord(evs[2 * c + edge], st));
+                return 0;
+            };
+            if (tm(0, 0, s) || k01(b_prev, b1, s) || tm(0, 1, s) || tm(1, 0, s) || k2(q_prev, q1, s) || tm(1, 1, s))
+                return -1;
+            OF3D_HIP(hipEventRecord(p->ev_chunk[c], s));
+            OF3D_HIP(hipStreamWaitEvent(s2, p->ev_chunk[c], 0));
+            if (tm(2, 0, s2) || k34(q_prev, q1, s2) || tm(2, 1, s2) || tm(4, 0, s2) || k5(o0, o1, q1, s2) ||
+                tm(4, 1, s2))
+                return -1;
+            b_prev = b1;
+            q_prev = q1;
+        }
+        OF3D_HIP(hipEventRecord(p->ev_join, s2));
+        OF3D_HIP(hipStreamWaitEvent(s, p->ev_join, 0));
+        if (!p->host_ev && p->timing_slots) {
+            p->tchunks[slot] = one_stage ? nch : 0;
+            ++p->tcount;
+        }
     }
-    OF3D_HIP(hipGetLastError());
-    OF3D_MARK(5);
     p->stages_run = kStages;
-    if (!p->host_ev && p->timing_slots) ++p->tcount;
-#undef OF3D_MARK
     return 0;
 }
 
@@ -608,6 +747,11 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     OF3D_HIP(hipMalloc(&p->X, 9 * p->fs * es));
     OF3D_HIP(hipMalloc(&p->Y, 9 * p->fs * es));
     OF3D_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    OF3D_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
+    OF3D_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    OF3D_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+    for (auto& e : p->ev_chunk) OF3D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (const char* e = getenv("OF3D_ZCHUNK")) p->zchunk = atoll(e);
     if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
         OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
         OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
@@ -631,6 +775,14 @@ void plan_free(of3d_plan* p) {
     for (auto& e : p->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto e : p->tev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {p->ev_fork, p->ev_join})
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : p->ev_chunk)
+        if (e) (void)hipEventDestroy(e);
+    if (p->stream2) {
+        (void)hipStreamSynchronize(p->stream2);
+        (void)hipStreamDestroy(p->stream2);
+    }
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }
@@ -849,9 +1001,12 @@ int of3d_plan_set_timing(of3d_plan* p, int slots) {
     if (slots < 0 || slots > 4096) return fail("of3d: timing slots must be in [0, 4096]");
     OF3D_HIP(hipSetDevice(p->device));
     if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
+    if (p->stream2) OF3D_HIP(hipStreamSynchronize(p->stream2));
     for (auto e : p->tev) (void)hipEventDestroy(e);
-    p->tev.assign((size_t)slots * (kStages + 1), nullptr);
+    p->tev_per_slot = std::max(kStages + 1, 2 * kMaxChunks);
+    p->tev.assign((size_t)slots * p->tev_per_slot, nullptr);
     for (auto& e : p->tev) OF3D_HIP(hipEventCreate(&e));
+    p->tchunks.assign(slots, 0);
     p->timing_slots = slots;
     p->tcount = 0;
     return 0;
@@ -876,7 +1031,17 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
     const int m = std::min(cap, kStages);
     std::vector<double> acc(kStages, 0.0);
     for (int64_t j = 0; j < n; ++j) {
-        hipEvent_t* e = &p->tev[(size_t)j * (kStages + 1)];
+        hipEvent_t* e = &p->tev[(size_t)j * p->tev_per_slot];
+        if (const int nch = p->tchunks[j]) {  // overlap mode: the one timed stage, summed over its chunks
+            const int st = __builtin_ctz(p->timing_mask);
+            OF3D_HIP(hipEventSynchronize(e[2 * nch - 1]));
+            for (int c = 0; c < nch; ++c) {
+                float t = 0.f;
+                OF3D_HIP(hipEventElapsedTime(&t, e[2 * c], e[2 * c + 1]));
+                acc[st] += t;
+            }
+            continue;
+        }
         int last = kStages;
         while (!((p->timing_mask >> (last - 1)) & 1u)) --last;  // closing boundary of the last timed stage
         OF3D_HIP(hipEventSynchronize(e[last]));
@@ -891,6 +1056,12 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
     if (p->k34.fn && m > 3) ms[3] = -1.0;  // fused K34: "prod_wy" holds W x too, "wx" is empty
     p->tcount = 0;
     return m;
+}
+
+int of3d_plan_set_overlap(of3d_plan* p, int64_t chunk_planes) {
+    if (!p) return fail("of3d: null plan");
+    p->zchunk = chunk_planes > 0 ? chunk_planes : 0;
+    return 0;
 }
 
 const char* of3d_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }

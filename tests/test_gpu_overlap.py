@@ -1,0 +1,82 @@
+"""Overlap mode (of3d_plan_set_overlap): the output planes in z chunks, the gradient stages
+of chunk c+1 on the caller's stream beside K34 + K5 of chunk c on the plan's second
+stream.  Every output bit-identical to the serial pipeline and (vx, vy, vz) to the oracle
+(oracle/cpu_ref.py, pinned to the reference's calc_flow3D, calc_flow.py:175-360), for
+whole volumes and for z sub-ranges (the z-slab path), chunk sizes that divide the range
+and ones that leave a ragged last chunk, and chunks thinner than the W-z halo."""
+import numpy as np
+import pytest
+
+from conftest import bits_equal
+from opticalflow3d_dev_amd import _lib, make_taps, radii
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_plan(img, s, t, w, chunk, z0=0, z1=None, mode=0, timing_stage=None):
+    import torch
+
+    dev = torch.device("cuda", 0)
+    nt, nz, ny, nx = img.shape
+    z1 = nz if z1 is None else z1
+    rt = radii(s, t, w)[2]
+    c = nt // 2
+    d_in = torch.from_numpy(np.ascontiguousarray(img[c - rt:c + rt + 1]).view(np.int16)).to(dev)
+    fp32 = bool(mode & _lib.OF3D_FP32)
+    vt = torch.float32 if fp32 else torch.float64
+    n = (z1 - z0) * ny * nx
+    outs = [torch.full((n,), float("nan"), dtype=vt, device=dev) for _ in range(3)]
+    rel = torch.full((n,), float("nan"), dtype=torch.float32, device=dev)
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=0, mode=mode, timing=4 if timing_stage else 0)
+    try:
+        plan.set_overlap(chunk)
+        if timing_stage:
+            plan.set_timing_stages([timing_stage])
+        plan.execute([d_in[i].data_ptr() for i in range(2 * rt + 1)], _lib.OF3D_U16, 0, z0, z1,
+                     outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), rel.data_ptr())
+        torch.cuda.synchronize(dev)
+        times = plan.stage_times() if timing_stage else None
+    finally:
+        plan.close()
+    shape = (z1 - z0, ny, nx)
+    return [o.cpu().numpy().reshape(shape) for o in outs] + [rel.cpu().numpy().reshape(shape)], times
+
+
+@pytest.mark.parametrize("chunk", [8, 13, 24])
+def test_overlap_whole_volume_bitwise(chunk):
+    s, t, w = 2, 2, 5
+    img = np.random.default_rng(40 + chunk).integers(0, 4096, size=(13, 48, 40, 56)).astype(np.uint16)
+    serial, _ = _run_plan(img, s, t, w, 0)
+    over, _ = _run_plan(img, s, t, w, chunk)
+    for a, b in zip(serial, over):
+        assert bits_equal(a, b)
+    st = cpu_ref.structure_tensor3d(img, s, t, w, backend="scipy")
+    for a, b in zip(over[:3], cpu_ref.solve3d(st)):
+        assert bits_equal(a, b)
+
+
+@pytest.mark.parametrize("z0,z1,chunk", [(10, 38, 8), (0, 20, 6), (30, 48, 5)])
+def test_overlap_subrange_bitwise(z0, z1, chunk):
+    s, t, w = 2, 3, 7  # c3 parameters: rw 21 > chunk
+    img = np.random.default_rng(z0 + z1).integers(0, 4096, size=(19, 48, 36, 44)).astype(np.uint16)
+    full, _ = _run_plan(img, s, t, w, 0)
+    over, _ = _run_plan(img, s, t, w, chunk, z0, z1)
+    for a, b in zip(full, over):
+        assert bits_equal(a[z0:z1], b)
+
+
+def test_overlap_fp32_equals_serial():
+    s, t, w = 2, 2, 5
+    img = np.random.default_rng(5).integers(0, 4096, size=(13, 40, 32, 64)).astype(np.uint16)
+    serial, _ = _run_plan(img, s, t, w, 0, mode=_lib.OF3D_FP32)
+    over, _ = _run_plan(img, s, t, w, 10, mode=_lib.OF3D_FP32)
+    for a, b in zip(serial, over):
+        assert bits_equal(a, b)
+
+
+def test_overlap_one_stage_timing():
+    s, t, w = 2, 2, 5
+    img = np.random.default_rng(6).integers(0, 4096, size=(13, 40, 32, 64)).astype(np.uint16)
+    out, times = _run_plan(img, s, t, w, 10, timing_stage="prod_wy")
+    assert set(times) == {"prod_wy"} and times["prod_wy"] > 0
