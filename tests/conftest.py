@@ -56,3 +56,29 @@ def bits_equal(a, b):
     a = np.ascontiguousarray(a)
     b = np.ascontiguousarray(b)
     return a.shape == b.shape and a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+def oracle3d(images, s, t, w):
+    """The oracle's vx, vy, vz and the fp64 eigenvalue range of its tensor
+    (the CPU restatement, scipy backend — tests only)."""
+    from oracle import cpu_ref
+
+    st = cpu_ref.structure_tensor3d(images, s, t, w, backend="scipy")
+    vx, vy, vz = cpu_ref.solve3d(st)
+    lmin, lmax = cpu_ref.eig_fp64_3d(st)
+    return vx, vy, vz, lmin, lmax
+
+
+def assert_rel_within(rel, lmin, lmax, tol):
+    """|rel - lambda_min| <= tol * |lambda_max| per voxel."""
+    err = np.abs(np.asarray(rel, np.float64) - lmin)
+    bad = err > tol * np.abs(lmax) + 1e-300
+    assert not bad.any(), f"{bad.sum()} voxels: max err/lmax {np.max(err / (np.abs(lmax) + 1e-300)):.3e}"
+
+
+def assert_flow3d_matches_oracle(out, images, s, t, w, rel_tol=1e-6):
+    """vx, vy, vz bit-identical to the oracle, rel within rel_tol * lambda_max."""
+    vx, vy, vz, lmin, lmax = oracle3d(images, s, t, w)
+    for got, want, name in zip(out[:3], (vx, vy, vz), ("vx", "vy", "vz")):
+        assert bits_equal(np.asarray(got, np.float64).reshape(want.shape), want), name
+    assert_rel_within(np.asarray(out[3]).reshape(lmin.shape), lmin, lmax, rel_tol)

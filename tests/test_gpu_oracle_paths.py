@@ -1,0 +1,142 @@
+"""The z-slab (configs[3]) and fp32 (configs[4]) paths checked directly
+against the reference's golden vectors and the oracle — not against the
+unsharded / fp64 HIP path (calc_flow.py:175-360).
+
+Tolerances:
+  * z-slabs: vx, vy, vz bit-identical to the golden vectors / oracle, rel
+    within 1e-6 * lambda_max of the reference's complex64 rel.
+  * fp32 path: max|dv| <= 1e-4 * max|v_ref| against the reference's fp64
+    vx/vy/vz; rel within 1e-4 * max|rel_ref| (float32 tensor, fp64 solve).
+"""
+import multiprocessing as mp
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import assert_flow3d_matches_oracle, assert_rel_within, bits_equal, golden_cases, load_golden, oracle3d
+from opticalflow3d_dev_amd import _lib, calc_flow2D_fp32, calc_flow3D_fp32
+from opticalflow3d_dev_amd.shard import flow3d_zslabs_host
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+ZSLAB_GOLDEN = ["c3d_rand_c2params", "c3d_rand_c3params", "c3d_nz1", "c3d_nz2", "c3d_nz3", "c3d_nz4",
+                "c3d_default_params", "c3d_smooth_translate", "c3d_frac_sigmas"]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("name", ZSLAB_GOLDEN)
+def test_zslabs_vs_golden(name, world):
+    """Slabs of `world` virtual ranks (thinner than the halo for most cases,
+    empty ones for Nz < world) against the reference's own outputs."""
+    g = load_golden(name)
+    vx, vy, vz, rel = flow3d_zslabs_host(g["images"], g["sig"], g["tsig"], g["wsig"], world)
+    assert bits_equal(vx, g["vx"]) and bits_equal(vy, g["vy"]) and bits_equal(vz, g["vz"])
+    assert_rel_within(rel, g["lmin64"], g["lmax64"], 1e-6)
+    err = np.abs(rel.astype(np.float64) - g["rel"].astype(np.float64))
+    assert np.all(err <= 1e-6 * np.abs(g["lmax64"]) + 1e-300)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_zslabs_seeded_vs_oracle(world):
+    img = np.random.default_rng(40 + world).integers(0, 4096, size=(13, 40, 64, 64)).astype(np.uint16)
+    out = flow3d_zslabs_host(img, 2, 2, 5, world)
+    assert_flow3d_matches_oracle(out, img, 2, 2, 5)
+
+
+def _zslab_worker(rank, world, port, q, img, sig):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd.shard import ZSlabFlow
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nt, nz, ny, nx = img.shape
+        dev = torch.device("cuda", 0)
+        zf = ZSlabFlow(nz, ny, nx, *sig, rank, world, device=0)
+        own = zf.allocate(torch.int16, dev)
+        c, rt = nt // 2, zf.rt
+        own.copy_(torch.from_numpy(np.ascontiguousarray(img[c - rt:c + rt + 1, zf.z0:zf.z1]).view(np.int16)))
+        n = (zf.z1 - zf.z0) * ny * nx
+        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
+        rel = torch.empty(n, dtype=torch.float32, device=dev)
+        zf.run(_lib.OF3D_U16, *outs, rel, torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        q.put((rank, zf.z0, zf.z1, [t.cpu().numpy() for t in outs + [rel]]))
+        zf.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zslab_gloo_two_ranks_vs_oracle():
+    """Two real processes, each holding only its own planes and exchanging
+    halos over gloo: the union of the slabs equals the oracle bit for bit."""
+    img = np.random.default_rng(9).integers(0, 4096, size=(13, 36, 24, 28)).astype(np.uint16)
+    sig = (2, 2, 5)
+    vx, vy, vz, lmin, lmax = oracle3d(img, *sig)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_zslab_worker, args=(r, 2, port, q, img, sig)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    covered = 0
+    for rank, z0, z1, outs in res:
+        covered += z1 - z0
+        shp = (z1 - z0, 24, 28)
+        for got, want in zip(outs[:3], (vx, vy, vz)):
+            assert bits_equal(got.reshape(shp), want[z0:z1])
+        assert_rel_within(outs[3].reshape(shp), lmin[z0:z1], lmax[z0:z1], 1e-6)
+    assert covered == 36
+
+
+FP32_TOL = 1e-4
+
+
+def _assert_fp32_close(got, want_v, want_rel):
+    for name, a, b in zip(("vx", "vy", "vz"), want_v, got[:len(want_v)]):
+        assert b.dtype == np.float32 and b.shape == a.shape
+        err = np.abs(b.astype(np.float64) - a).max()
+        assert err <= FP32_TOL * np.abs(a).max(), (name, err, np.abs(a).max())
+    rel = got[len(want_v)].astype(np.float64)
+    want_rel = np.asarray(want_rel, np.float64)
+    assert np.abs(rel - want_rel).max() <= FP32_TOL * np.abs(want_rel).max()
+
+
+def _smooth(shape, seed):
+    return cpu_ref.synthetic_stack_np(shape, seed=seed)
+
+
+@pytest.mark.parametrize("name", ["c3d_smooth_translate", "c3d_float32_nt11", "c3d_rand_c2params",
+                                  "c3d_rand_c3params", "c3d_default_params", "c3d_flat"])
+def test_fp32_3d_vs_golden(name):
+    g = load_golden(name)
+    got = calc_flow3D_fp32(g["images"], g["sig"], g["tsig"], g["wsig"])
+    _assert_fp32_close(got, (g["vx"], g["vy"], g["vz"]), g["rel"])
+
+
+@pytest.mark.parametrize("name", ["c2d_smooth_translate", "c2d_c1params", "c2d_c2params", "c2d_float32"])
+def test_fp32_2d_vs_golden(name):
+    g = load_golden(name)
+    got = calc_flow2D_fp32(g["images"], g["sig"], g["tsig"], g["wsig"])
+    _assert_fp32_close(got, (g["vx"], g["vy"]), g["rel"])
+
+
+@pytest.mark.parametrize("shape,sig", [((13, 24, 48, 56), (2, 2, 5)), ((19, 16, 40, 44), (2, 3, 7))])
+def test_fp32_3d_vs_oracle(shape, sig):
+    img = _smooth(shape, 31)
+    vx, vy, vz, lmin, lmax = oracle3d(img, *sig)
+    got = calc_flow3D_fp32(img, *sig)
+    _assert_fp32_close(got, (vx, vy, vz), lmin)

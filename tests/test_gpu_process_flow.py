@@ -6,7 +6,7 @@ import re
 import numpy as np
 import pytest
 
-from conftest import bits_equal
+from conftest import assert_flow3d_matches_oracle, assert_rel_within, bits_equal, oracle3d
 from opticalflow3d_dev_amd import process_flow
 from opticalflow3d_dev_amd import tiff as tf
 from oracle import cpu_ref
@@ -27,13 +27,9 @@ def test_onetif_3d(tmp_path, capsys):
     files = sorted(p.name for p in out.glob("*.tiff"))
     assert files == sorted(f"cells_{n}_t{t:04d}.tiff" for n in ("vx", "vy", "vz", "rel") for t in (3, 4, 5))
     for hh in range(3):
-        ref = cpu_ref.calc_flow3D(stack[hh:hh + 7], 1, 1, 2, backend="scipy")
-        for name, r in zip(("vx", "vy", "vz", "rel"), ref):
-            got = tf.imread(out / f"cells_{name}_t{hh + 3:04d}.tiff")
-            if name == "rel":
-                assert got.dtype == np.float32 and got.shape == r.shape
-            else:
-                assert bits_equal(got, r)
+        got = [tf.imread(out / f"cells_{name}_t{hh + 3:04d}.tiff") for name in ("vx", "vy", "vz", "rel")]
+        assert got[3].dtype == np.float32 and got[3].shape == (5, 20, 24)
+        assert_flow3d_matches_oracle(got, stack[hh:hh + 7], 1, 1, 2)
     text = capsys.readouterr().out
     assert "Note: regardless of input filenames, the first image = frame 0." in text
     assert len(re.findall(r"No data will be saved for frame", text)) == 6
@@ -60,8 +56,8 @@ def test_sequencet_3d_natural_order(tmp_path):
         tf.imwrite(tmp_path / f"v_t{t * 5}.tif", stack[t])  # t0, t5, t10, ... natural order != ASCII order
     process_flow(str(tmp_path), "v_t.*", "SequenceT", 3, 1, 1, 2)
     out = tmp_path / "OpticalFlow3D" / "v_t"
-    ref = cpu_ref.calc_flow3D(stack, 1, 1, 2, backend="scipy")
-    assert bits_equal(tf.imread(out / "v_t_vx_t0003.tiff"), ref[0])
+    got = [tf.imread(out / f"v_t_{name}_t0003.tiff") for name in ("vx", "vy", "vz", "rel")]
+    assert_flow3d_matches_oracle(got, stack, 1, 1, 2)
 
 
 def test_stdout_order(tmp_path, capsys):
@@ -81,7 +77,6 @@ def test_stdout_order(tmp_path, capsys):
 def test_flowstream_ring_wraps(ndim, dtype, d2h):
     """Many frames through the device ring (wraps it several times, every
     buffer set reused) — each output equals calc_flow3D/2D of its window."""
-    from opticalflow3d_dev_amd import calc_flow2D, calc_flow3D
     from opticalflow3d_dev_amd.stream import FlowStream
 
     tsig = 2 if ndim == 3 else 1
@@ -97,18 +92,22 @@ def test_flowstream_ring_wraps(ndim, dtype, d2h):
                 pend.append((t - nwin + 1, fs.submit()))
                 if len(pend) == fs.depth:  # keep every buffer set in flight
                     k, p = pend.pop(0)
-                    _check_stream(p, stack[k:k + nwin], ndim, tsig, calc_flow2D, calc_flow3D)
+                    _check_stream(p, stack[k:k + nwin], ndim, tsig)
         for k, p in pend:
-            _check_stream(p, stack[k:k + nwin], ndim, tsig, calc_flow2D, calc_flow3D)
+            _check_stream(p, stack[k:k + nwin], ndim, tsig)
     finally:
         fs.close()
 
 
-def _check_stream(p, win, ndim, tsig, f2, f3):
-    ref = f3(win, 1, tsig, 2) if ndim == 3 else f2(win, 1, tsig, 2)
+def _check_stream(p, win, ndim, tsig):
+    """One ring output against the oracle of its window."""
     got = p.result()
-    for g, r in zip(got, ref):
-        assert bits_equal(g, r)
+    win = np.asarray(win).astype(np.asarray(win).dtype.newbyteorder("="))
+    if ndim == 3:
+        assert_flow3d_matches_oracle(got, win, 1, tsig, 2)
+    else:
+        for g, r in zip(got, cpu_ref.calc_flow2D(win, 1, tsig, 2, backend="scipy")):
+            assert bits_equal(g, r)
     p.release()
 
 
@@ -159,6 +158,11 @@ def test_matlab_output_mode(tmp_path):
     ref = cf._flow3d(stack[0:7], 1, 1, 2, rel_fp64=True)
     raw = (out / "m_vx_t0003.tiff").read_bytes()
     assert raw[:4] == b"II+\x00"  # BigTIFF
+    got = []
     for name, r in zip(("vx", "vy", "vz", "rel"), ref):
-        got = tf.imread_libtiff(out / f"m_{name}_t0003.tiff")
-        assert got.dtype == np.float64 and bits_equal(got, r)
+        got.append(tf.imread_libtiff(out / f"m_{name}_t0003.tiff"))
+        assert got[-1].dtype == np.float64 and bits_equal(got[-1], r)
+    vx, vy, vz, lmin, lmax = oracle3d(stack[0:7], 1, 1, 2)
+    for g, want in zip(got[:3], (vx, vy, vz)):
+        assert bits_equal(g, want)
+    assert_rel_within(got[3], lmin, lmax, 1e-10)  # fp64 rel vs fp64 eigvalsh
