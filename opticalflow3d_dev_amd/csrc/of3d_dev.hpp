@@ -1140,6 +1140,298 @@ __global__ __launch_bounds__(256, 3) void k_grad_xy_c(const T* __restrict__ Ic, 
     }
 }
 
+// 16-byte global -> LDS copy (LDS-DMA): lane i's 16 bytes land at lds_byte + 16 i.
+// Inline asm keeps it out of the compiler's wait bookkeeping (the compiler
+// would drain it with vmcnt(0) before every LDS read); waits are explicit.
+__device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_byte)
+                 : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// K12: the gradient y, x and z passes in one kernel (calc_flow.py:279-288) — the four
+// pre-z fields never leave the CU (K1c + K2c write and re-read them through HBM).
+// Block = TY = 4 rows x TX = 128 - 2 RD output columns (128 staged columns: two waves per
+// row), marching a chunk of output planes.  Wave w: half h = w & 1 (staged column
+// c = 64 h + lane), role / row r = w >> 1.  Per input plane (one step):
+//   staging (LDS-DMA): the plane's TY + 2 RD rows of dt0 and of the centre frame I (the
+//     block's staged columns, 16-byte granules) go straight into LDS, a chunk of K (3, or 2
+//     where LDS is short) planes at a time, two chunks ahead (2 K plane slots): one chunk's loads
+//     stay in flight while the previous chunk computes; one vmcnt(0) per chunk;
+//   y passes (LDS -> registers): role 0 A1 = y(G)[dt0], role 1 A2 = y(D)[I], role 2
+//     A3 = y(S)[I] of the thread's staged column (clamped at the global edge), results
+//     into LDS tiles (two buffers);
+//   x passes (LDS): thread (row r, staged column c) forms B1 = x(G)[A1], B2 = x(S)[A2],
+//     B3 = x(D)[A3], B4 = x(S)[A3] for output column c - RD (lanes past the block's
+//     outputs compute clamped duplicates and store nothing);
+//   z passes (registers): B1..B4 enter per-thread register rings (NR = 2 RD + 2 slots for
+//     the radius-RD fields, NRS = RD + 1 for the smooth ones; compile-time slots: the plane
+//     loop is unrolled by NR); dt = z(G)[B1] and dz = z(D)[B4] leave once plane q + RD is
+//     in, dy = z(S)[B2] and dx = z(S)[B3] once plane q + RS is.
+// One barrier per step; the y passes of step s + 1 run beside the x / z passes of step s
+// (the A tiles alternate), so each wave has two independent streams of work per step.
+// Same expression order as K1c + K2c (scipy's), staged rows/columns clamped at the global
+// edge, planes clamped to [0, nzc): bit-identical.  Blocks are numbered XCD-aware (the
+// tiles of one XCD form a band of rows, so the halo rows of neighbouring tiles share an L2).
+// Needs nx * sizeof(F) and nx * sizeof(T) multiples of 16 bytes and 16-byte aligned planes.
+// ---------------------------------------------------------------------------
+constexpr int K12_TY = 4;  // rows per block
+#ifndef OF3D_K12_EXP
+#define OF3D_K12_EXP 0  // experiments: 1 = no gradient stores, 2 = no chunk waits (timing only)
+#endif
+template <int RD>
+__host__ __device__ constexpr int k12_tx() { return 128 - 2 * RD; }
+// LDS bytes of one staged plane: NRW rows of dt0 (128 + EPL columns) and of I (128 + EPL_T)
+template <typename T, typename F, int RD>
+__host__ __device__ constexpr int k12_slot_granules() {
+    return (K12_TY + 2 * RD) * ((128 * (int)sizeof(F)) / 16 + 1 + (128 * (int)sizeof(T)) / 16 + 1);
+}
+template <typename T, typename F, int RD>
+__host__ __device__ constexpr int k12_slot_bytes() { return ((k12_slot_granules<T, F, RD>() + 63) / 64) * 1024; }
+// A tiles: [2 buffers][3 fields][even / odd copy][TY][K12_AP]; the odd copy is the row
+// shifted by one element, so every x-pass window starts 16-byte aligned in one of the two
+// (pairs read as ds_read_b128: 4 LDS cycles per 16 B; ds_read2_b64 costs 16).  Pitch
+// 132: the odd copy sits 128 B (mod 256) from the even one (conflict-free b128 groups).
+constexpr int K12_AP = 132;
+template <typename F>
+__host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * K12_AP * (int)sizeof(F); }
+// planes per DMA chunk: 3 where two chunks of slots + the A tiles fit 160 KiB, else 2
+template <typename T, typename F, int RD>
+__host__ __device__ constexpr int k12_k() {
+    return 6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 3 : 2;
+}
+template <typename T, typename F, int RD>
+__host__ __device__ constexpr int k12_lds_bytes() {
+    return 2 * k12_k<T, F, RD>() * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>();
+}
+
+template <typename T, typename F, int RD, int RS>
+__global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict__ Ic, const F* __restrict__ D0,
+                                                             int zin0, int nzc, int ny, int nx, DevTaps<F> tp,
+                                                             F* __restrict__ G, size_t fs, int zg0, int q0, int nq,
+                                                             int zc, int ntile, int nbx) {
+    constexpr int TY = K12_TY, TX = k12_tx<RD>(), NRW = TY + 2 * RD;
+    constexpr int NR = 2 * RD + 2, NRS = RD + 1, AP = K12_AP;  // ring slots; A tile pitch
+    constexpr int AF = 2 * TY * AP, AB = 3 * AF;  // A field stride (even + odd copy), buffer stride
+    static_assert(NRS >= 2 * RS + 1 && NR % NRS == 0 && NR % 2 == 0 && TX >= 8, "K12 geometry");
+    constexpr int EF = 16 / (int)sizeof(F), ET = 16 / (int)sizeof(T);  // elements per granule
+    constexpr int GD = 128 / EF + 1, GI = 128 / ET + 1;                 // granules per staged row
+    constexpr int NG = NRW * (GD + GI), NJ = (NG + 63) / 64;            // granules / DMA instrs per plane
+    constexpr int K = k12_k<T, F, RD>();  // planes per DMA chunk
+    constexpr int SLOT = k12_slot_bytes<T, F, RD>(), NSLOT = 2 * K;
+    static_assert(k12_lds_bytes<T, F, RD>() <= 160 * 1024, "K12 LDS");
+    constexpr int NJW = (NJ + 7) / 8;                                   // DMA instrs per wave per plane
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* At = reinterpret_cast<F*>(smem_raw + NSLOT * SLOT);  // [2 buffers][3 fields][even, odd][TY][AP]
+    const int t = threadIdx.x, lane = t & 63;
+    const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int role = w >> 1, c = 64 * (w & 1) + lane;
+    const int per = (ntile + 7) >> 3;
+    const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    if (tile >= ntile) return;  // block-uniform
+    const int by = tile / nbx, bx = tile - by * nbx;
+    const int y0 = by * TY, x0 = bx * TX;
+    const int qa = q0 + (int)blockIdx.y * zc, nout = min(zc, q0 + nq - qa);
+    const size_t plane = (size_t)ny * nx;
+    // staged columns: dt0 from gd0, I from gi0 (granule-aligned starts of the block's window)
+    const int xs = max(x0 - RD, 0);
+    const int gd0 = xs / EF * EF, gi0 = xs / ET * ET;
+    const int gc = clampi(x0 - RD + c, 0, nx - 1);  // this thread's staged column (y passes)
+    const int pd = gc - gd0, pi = gc - gi0;         // its LDS positions in the dt0 / I rows
+    // DMA sources of this wave's instructions (plane-relative element offsets): instruction
+    // j = w + 8 i covers granules 64 j .. 64 j + 63 of the slot (dt0 rows, then I rows)
+    unsigned doff[NJW];
+    bool isd[NJW];
+#pragma unroll
+    for (int i = 0; i < NJW; ++i) {
+        const int g = min(64 * (w + 8 * i) + lane, NG - 1);
+        if (g < NRW * GD) {
+            const int r = g / GD, q = g - r * GD;
+            isd[i] = true;
+            doff[i] = (unsigned)clampi(y0 - RD + r, 0, ny - 1) * (unsigned)nx + (unsigned)min(gd0 + q * EF, nx - EF);
+        } else {
+            const int gg = g - NRW * GD, r = gg / GI, q = gg - r * GI;
+            isd[i] = false;
+            doff[i] = (unsigned)clampi(y0 - RD + r, 0, ny - 1) * (unsigned)nx + (unsigned)min(gi0 + q * ET, nx - ET);
+        }
+    }
+    const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
+    const int nsteps = nout + 2 * RD;
+    auto issue_plane = [&](int s) {  // DMA of step s's plane into slot s % NSLOT
+        const size_t pz = (size_t)(clampi(qa - RD + s, 0, nzc - 1) - zin0) * plane;
+        const unsigned sb = lds0 + (unsigned)((s % NSLOT) * SLOT);
+#pragma unroll
+        for (int i = 0; i < NJW; ++i) {
+            if (w + 8 * i < NJ) {
+                const void* src = isd[i] ? (const void*)(D0 + pz + doff[i]) : (const void*)(Ic + pz + doff[i]);
+                glds16(src, __builtin_amdgcn_readfirstlane(sb + (unsigned)((w + 8 * i) * 1024)));
+            }
+        }
+    };
+    auto issue_chunk = [&](int m) {
+        for (int s = m * K; s < min((m + 1) * K, nsteps); ++s) issue_plane(s);
+    };
+    F hg[RD + 1], hd[RD + 1], hs[RS + 1];
+#pragma unroll
+    for (int k = 0; k <= RD; ++k) hg[k] = tp.g[k], hd[k] = tp.d[k];
+#pragma unroll
+    for (int k = 0; k <= RS; ++k) hs[k] = tp.s[k];
+    // x / z passes: output column x0 + c - RD (reads clamped into the block's outputs);
+    // stores of lanes outside the volume are skipped
+    const int cx = clampi(c, RD, RD + TX - 1);
+    const int xo = x0 + c - RD, yo = y0 + role;
+    const bool st_ok = c >= RD && c < RD + TX && xo < nx && yo < ny;
+    constexpr unsigned ES = sizeof(F);
+    const unsigned vout = (unsigned)(xo < 0 ? 0 : xo) * ES, sout = (unsigned)(yo < ny ? yo : 0) * (unsigned)nx * ES;
+    F r1[NR], r2[NRS], r3[NRS], r4[NR];  // z rings of B1 .. B4
+    // ---- y passes of step s (roles 0..2): staged rows of slot s % NSLOT -> A tile s & 1 ----
+    auto ypass_step = [&](int s, int par) {
+        F* A = At + par * AB;
+        const unsigned char* slot = smem_raw + (s % NSLOT) * SLOT;
+        auto ypass = [&]<int R, bool ANTI, bool DT>(const F(&h)[R + 1]) {
+            F v[NRW];
+            if constexpr (DT) {
+                const F* rd_ = reinterpret_cast<const F*>(slot) + pd;
+#pragma unroll
+                for (int i = 0; i < NRW; ++i) v[i] = rd_[i * GD * EF];
+            } else {
+                const T* ri_ = reinterpret_cast<const T*>(slot + NRW * GD * 16) + pi;
+#pragma unroll
+                for (int i = 0; i < NRW; ++i) v[i] = (F)ri_[i * GI * ET];
+            }
+            F* a = A + role * AF + c;  // even copy at c, odd copy at c - 1
+#pragma unroll
+            for (int r = 0; r < TY; ++r) {
+                F o = v[r + RD] * h[0];
+#pragma unroll
+                for (int k = R; k >= 1; --k)
+                    o = o + (ANTI ? (v[r + RD - k] - v[r + RD + k]) : (v[r + RD - k] + v[r + RD + k])) * h[k];
+                a[r * AP] = o;
+                if (c > 0) a[TY * AP + r * AP - 1] = o;
+            }
+        };
+        if (role == 0)
+            ypass.template operator()<RD, false, true>(hg);
+        else if (role == 1)
+            ypass.template operator()<RD, true, false>(hd);
+        else if (role == 2)
+            ypass.template operator()<RS, false, false>(hs);
+    };
+    // Schedule (one barrier per step; the y passes of step s + 1 run beside the x / z passes
+    // of step s, in the other A buffer):
+    //   prologue: chunk 0 loaded; chunk 1 issued; y(0)
+    //   step s:   [last step of a chunk: vmcnt(0) — retires the next chunk's DMA, issued a
+    //             chunk ago] barrier [then: issue the chunk after it into the slots of the
+    //             chunk just finished] x / z (s), y (s + 1)
+    issue_chunk(0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    issue_chunk(1);
+    ypass_step(0, 0);
+    for (int u0 = 0; u0 < nsteps; u0 += NR) {
+        bool done = false;
+        [&]<int... J>(std::integer_sequence<int, J...>) {
+            (
+                [&] {
+                    if (done) return;
+                    constexpr int j = J;
+                    const int s = u0 + j;
+                    const bool chunk_end = s % K == K - 1;
+#if OF3D_K12_EXP != 2
+                    if (chunk_end) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+                    lds_barrier();
+                    if (chunk_end) {
+                        const int m2 = s / K + 2;
+                        if (m2 * K < nsteps) issue_chunk(m2);
+                    }
+                    // ---- x passes: thread (row `role`, staged column cx) of A tile s & 1 ----
+                    // window [cx - R, cx + R] of a field row, as 16-byte pairs from the copy
+                    // where it starts aligned
+                    const F* arow = At + (j & 1) * AB + role * AP;  // NR even: parity of s
+                    auto window = [&]<int R>(int f, F (&x)[2 * R + 2]) {
+                        const int st = cx - R;
+                        const F* q = arow + f * AF + ((st & 1) ? TY * AP + st - 1 : st);
+                        typedef F F2 __attribute__((ext_vector_type(2)));
+                        const F2* q2 = reinterpret_cast<const F2*>(__builtin_assume_aligned(q, 2 * sizeof(F)));
+#pragma unroll
+                        for (int i = 0; i <= R; ++i) {
+                            const F2 v2 = q2[i];
+                            x[2 * i] = v2.x;
+                            x[2 * i + 1] = v2.y;
+                        }
+                    };
+                    F x1[2 * RD + 2], x2[2 * RS + 2], x3[2 * RD + 2];
+                    window.template operator()<RD>(0, x1);
+                    window.template operator()<RS>(1, x2);
+                    window.template operator()<RD>(2, x3);
+                    F b1 = x1[RD] * hg[0], b2 = x2[RS] * hs[0], b3 = x3[RD] * hd[0], b4 = x3[RD] * hs[0];
+#pragma unroll
+                    for (int k = RD; k >= 1; --k) {
+                        b1 = b1 + (x1[RD - k] + x1[RD + k]) * hg[k];
+                        b3 = b3 + (x3[RD - k] - x3[RD + k]) * hd[k];
+                    }
+#pragma unroll
+                    for (int k = RS; k >= 1; --k) {
+                        b2 = b2 + (x2[RS - k] + x2[RS + k]) * hs[k];
+                        b4 = b4 + (x3[RD - k] + x3[RD + k]) * hs[k];
+                    }
+                    r1[j % NR] = b1;
+                    r4[j % NR] = b4;
+                    r2[j % NRS] = b2;
+                    r3[j % NRS] = b3;
+                    // ---- y passes of the next step (independent work for the scheduler) ----
+                    if (s + 1 < nsteps) ypass_step(s + 1, (j + 1) & 1);
+                    // ---- z passes ----
+                    auto slotz = [](int i, int n) { return ((i % n) + n) % n; };
+                    if (s >= 2 * RD) {  // plane q = qa + s - 2 RD: dt and dz
+                        const int q = qa + s - 2 * RD;
+                        constexpr int cz = j - RD;
+                        F o1 = r1[slotz(cz, NR)] * hg[0], o4 = r4[slotz(cz, NR)] * hd[0];
+#pragma unroll
+                        for (int k = RD; k >= 1; --k) {
+                            o1 = o1 + (r1[slotz(cz - k, NR)] + r1[slotz(cz + k, NR)]) * hg[k];
+                            o4 = o4 + (r4[slotz(cz - k, NR)] - r4[slotz(cz + k, NR)]) * hd[k];
+                        }
+#if OF3D_K12_EXP != 1
+                        if (st_ok) {
+                            const size_t pq = (size_t)(q - zg0) * plane;
+                            buf_st<F>(o1, buf_rsrc(G + pq), vout, sout);
+                            buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vout, sout);
+                        }
+#else
+                        if (o1 == 12345.0 && o4 == 1.0) G[0] = 0;
+#endif
+                    }
+                    if (s >= RD + RS && s < nout + RD + RS) {  // plane q = qa + s - RD - RS: dy and dx
+                        const int q = qa + s - RD - RS;
+                        constexpr int cz = j - RS;
+                        F o2 = r2[slotz(cz, NRS)] * hs[0], o3 = r3[slotz(cz, NRS)] * hs[0];
+#pragma unroll
+                        for (int k = RS; k >= 1; --k) {
+                            o2 = o2 + (r2[slotz(cz - k, NRS)] + r2[slotz(cz + k, NRS)]) * hs[k];
+                            o3 = o3 + (r3[slotz(cz - k, NRS)] + r3[slotz(cz + k, NRS)]) * hs[k];
+                        }
+#if OF3D_K12_EXP != 1
+                        if (st_ok) {
+                            const size_t pq = (size_t)(q - zg0) * plane;
+                            buf_st<F>(o2, buf_rsrc(G + fs + pq), vout, sout);
+                            buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vout, sout);
+                        }
+#else
+                        if (o2 == 12345.0 && o3 == 1.0) G[1] = 0;
+#endif
+                    }
+                    if (s + 1 >= nsteps) done = true;
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NR>{});
+        if (done) break;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Solves.  Expression trees copied from calc_flow.py:337-340 (3D) and
 // :154-168 (2D); numpy's x**-1 is a correctly rounded reciprocal, x**2 = x*x.
@@ -1274,16 +1566,6 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve(const F* __restrict__ Q,
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
-// 16-byte global -> LDS copy (LDS-DMA): lane i's 16 bytes land at lds_byte + 16 i.
-// Inline asm keeps it out of the compiler's wait bookkeeping (the compiler
-// would drain it with vmcnt(0) before every LDS read); waits are explicit.
-__device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_byte)
-                 : "memory");
-}
 
 // K5 with LDS-DMA staging: the field windows are loaded straight into NB LDS
 // buffers, NB - 1 fields ahead of the pass (no staging registers, no VGPR cost

@@ -60,6 +60,7 @@ struct of3d_plan {
     size_t k5d_lds = 0;
     bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
     bool k2c = true;  // z-march K2 where instantiated (OF3D_K2C=0: k_grad_z)
+    bool k12 = true;  // fused gradient kernel where instantiated (OF3D_K12=0: K1c + K2c)
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
@@ -394,9 +395,13 @@ int set_attrs_t(of3d_plan* p) {
     if (rc) return -1;
     if (const char* e = getenv("OF3D_K1C"); e && e[0] == '0') p->k1c = false;
     if (const char* e = getenv("OF3D_K2C"); e && e[0] == '0') p->k2c = false;
-    for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32})
+    if (const char* e = getenv("OF3D_K12"); e && e[0] == '0') p->k12 = false;
+    for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32}) {
         if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
             OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        if (const void* f = k12_fn<F>(dt, p->rd, p->rs))
+            OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)k12_lds<F>(dt, p->rd)));
+    }
     if (k5c_setup<F>(p)) return -1;
     return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
 }
@@ -466,8 +471,22 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const size_t es = dtype_size(dtype);
     const int nwin = 2 * p->rt + 1;
     const int nf = d3 ? 9 : 5;
+    // K12 (fused gradient y/x/z passes, 3D): dt0 then lives in Y4 (K12 writes G = Y0..3
+    // while other blocks still read dt0 planes), the pre-z fields B are never formed
+    // (LDS-DMA staging: 16-byte rows and planes of dt0 and of the centre frame)
+    const bool k12_al = (nx * sizeof(F)) % 16 == 0 && (nx * es) % 16 == 0 &&
+                        ((uintptr_t)d_frames[p->rt] + (size_t)(R.zb0 - frame_z0) * plane * es) % 16 == 0;
+    // K12 pays where its blocks can march >= 32 planes and still fill the GPU (c2, 256^2 x 64:
+    // 16-plane marches re-form 12 halo planes each, K1c + K2c measured faster; c3: K12 0.62 vs
+    // 0.83 ms); OF3D_K12=1 forces it, OF3D_K12=0 disables it
+    const char* k12_env = getenv("OF3D_K12");
+    const int k12_tiles = (int)cdiv(nx, 128 - 2 * p->rd) * (int)cdiv(ny, K12_TY);
+    const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
+    const void* k12 = (d3 && p->k12 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
+                       (k12_big || (k12_env && k12_env[0] == '1')))
+                          ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
     // field buffers
-    F* D0b = Y;                        // temporal derivative (K0 -> K1), origin zb0
+    F* D0b = k12 ? Y + 4 * fs : Y;     // temporal derivative (K0 -> K1 / K12), origin zb0
     F* Bb = d3 ? Y + 4 * fs : X;       // pre-z fields (3D) / final gradients (2D), origin zb0
     const F* Gb = d3 ? Y : X;          // gradients, origin zg0
     F* Pb = d3 ? X : Y;                // K3 W-y (fallback) / K34 W-xy
@@ -508,6 +527,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&D0};
             OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
         }
+        if (k12) return 0;  // the y / x passes run inside K12 (stage grad_z)
         const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
         const F* D0c = D0;
         F* Bo = Bb + (size_t)(b0 - R.zb0) * plane;
@@ -544,6 +564,30 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     auto k2 = [&](int64_t q0, int64_t q1, hipStream_t st) -> int {
         if (q1 <= q0 || !d3) return 0;
         const int ng = (int)(q1 - q0);
+        if (k12) {
+            // K12 over output planes [q0, q1): the centre frame and dt0 from plane zb0 on
+            const void* Ic = (const char*)d_frames[p->rt] + (size_t)(R.zb0 - frame_z0) * plane * es;
+            const F* D0c = D0b;
+            F* Go = Y;
+            const int tx = p->rd == 3 ? k12_tx<3>() : (p->rd == 6 ? k12_tx<6>() : k12_tx<9>());
+            int nbx = (int)cdiv(nx, tx), ntile = nbx * (int)cdiv(ny, K12_TY);
+            int zin0 = (int)R.zb0, nzc = (int)R.zb1, zg0 = (int)R.zg0, qa = (int)q0, nq = ng;
+            // planes per block: the longest march that still gives >= 1024 blocks (each march
+            // re-forms 2 rd halo planes), at least 16
+            static const int zc_env = getenv("OF3D_K12_ZC") ? atoi(getenv("OF3D_K12_ZC")) : 0;
+            int zc = zc_env;
+            if (zc <= 0) {
+                zc = 64;
+                while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;
+            }
+            const unsigned gx = 8 * cdiv(ntile, 8);
+            const size_t lds = k12_lds<F>(dtype, p->rd);
+            void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&zin0, (void*)&nzc, (void*)&ny, (void*)&nx, (void*)&tp,
+                            (void*)&Go, (void*)&fs, (void*)&zg0, (void*)&qa, (void*)&nq, (void*)&zc, (void*)&ntile,
+                            (void*)&nbx};
+            OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(128 * K12_TY), args, lds, st));
+            return 0;
+        }
         const void* k2c = nullptr;
         if (p->k2c) {
             if (p->rd == 6 && p->rs == 2) k2c = (const void*)k_grad_z_c<F, 6, 2>;

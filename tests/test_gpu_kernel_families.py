@@ -14,10 +14,10 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12")
 
 
-def _run(img, s, t, w, ndim, mode, old):
+def _run(img, s, t, w, ndim, mode, old, force=None):
     import torch
 
     saved = {k: os.environ.get(k) for k in FAMILY_ENV}
@@ -27,6 +27,7 @@ def _run(img, s, t, w, ndim, mode, old):
                 os.environ[k] = "0"
             else:
                 os.environ.pop(k, None)
+        os.environ.update(force or {})
         dev = torch.device("cuda", 0)
         nt = img.shape[0]
         vol = img.shape[1:] if ndim == 3 else (1,) + img.shape[1:]
@@ -76,6 +77,21 @@ def test_families_bit_identical(case, fp32):
         img = img[:, 0]
     mode = _lib.OF3D_FP32 if fp32 else 0
     new = _run(img, s, t, w, ndim, mode, old=False)
+    ref = _run(img, s, t, w, ndim, mode, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", range(3))
+@pytest.mark.parametrize("fp32", [False, True])
+def test_fused_gradients_k12_forced(case, fp32):
+    """K12 (fused y/x/z gradient passes) forced on volumes below its size heuristic, against
+    K1c + K2c and the older kernels: every output bit-identical."""
+    shape, (s, t, w), ndim = CASES[case]
+    rng = np.random.default_rng(400 + case)
+    img = rng.integers(0, 4096, size=shape).astype(np.uint16)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    new = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_K12": "1"})
     ref = _run(img, s, t, w, ndim, mode, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))

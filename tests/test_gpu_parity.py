@@ -140,3 +140,19 @@ def test_deterministic():
     b = calc_flow3D(img, 1, 1, 3)
     for x, y in zip(a, b):
         assert bits_equal(x, y)
+
+
+@pytest.mark.parametrize("name", golden_cases("c3d"))
+def test_golden_3d_fused_gradients(name, monkeypatch):
+    """K12 (the fused y/x/z gradient kernel) forced on: still bit-identical to the reference."""
+    monkeypatch.setenv("OF3D_K12", "1")
+    g = load_golden(name)
+    vx, vy, vz, rel = calc_flow3D(g["images"], g["sig"], g["tsig"], g["wsig"])
+    assert bits_equal(vx, g["vx"]) and bits_equal(vy, g["vy"]) and bits_equal(vz, g["vz"])
+    assert_rel_close(rel, g["rel"], g["lmax64"], REL_TOL_REF)
+
+
+@pytest.mark.parametrize("case", range(len(SEEDED_3D)))
+def test_seeded_3d_fused_gradients(case, monkeypatch):
+    monkeypatch.setenv("OF3D_K12", "1")
+    test_seeded_3d_vs_oracle(case)
