@@ -170,8 +170,19 @@ def _now():
     return str(datetime.now())
 
 
+def _dist_context():
+    """(rank, world) of an initialised torch.distributed job, else (0, 1)."""
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return 0, 1
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSig=3, tSig=1, wSig=4,
-                 precision="fp64", matlab_output=False):
+                 precision="fp64", matlab_output=False, parallel="auto"):
     """Parse a TIFF time lapse, run the flow per output frame, write TIFFs.
 
     Mirrors calc_flow.py:362-625: same checks and messages, the same
@@ -181,7 +192,17 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     (configs[4]) runs the float32 path and writes float32 TIFFs;
     matlab_output=True writes what the reference's MATLAB twin writes
     (M/TIFFwrite.m: LZW BigTIFF, float64; rel kept fp64 as pageeig does,
-    M/calc_flow3D.m:235-236)."""
+    M/calc_flow3D.m:235-236).
+
+    Several GPUs (one process per GPU, torch.distributed initialised, e.g. by
+    ``shard.init_distributed()`` under torchrun): the reference's own parallel axis
+    (calc_flow.py:512, "this could become a parfor loop") — ``parallel="frames"``: each
+    rank streams a contiguous block of output frames and writes their files;
+    ``parallel="zslab"`` (3D): every rank reads only its z-planes of each frame, fetches
+    the stencil halo planes from its z-neighbours (RCCL P2P) and writes its planes of
+    every output file (shard, tiff.write_planes; no gather).  ``"auto"``: frames when
+    there are at least as many output frames as ranks, else z-slabs.  Files and pixel
+    values are the same as on one GPU."""
     ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
     imDir = Path(imDir)
     if not imDir.is_dir():
@@ -231,56 +252,80 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
         NtChunk = NtChunk + 1
     NtSlice = math.ceil(NtChunk / 2) - 1
 
+    rank, world = _dist_context()
     savedir = imDir / ('OpticalFlow3D' if spatialDimensions == 3 else 'OpticalFlow2D')
     savedir.mkdir(exist_ok=True)
     imNameSave = imName.replace('.*', '')
     savedir = savedir / imNameSave
     savedir.mkdir(exist_ok=True)
-    _write_parameters(savedir / (imNameSave + '_parameters.csv'), xyzSig, tSig, wSig, Nx, Ny, Nz, Nt)
+    if rank == 0:
+        _write_parameters(savedir / (imNameSave + '_parameters.csv'), xyzSig, tSig, wSig, Nx, Ny, Nz, Nt)
 
     ### Processing Loop (calc_flow.py:497-625)
-    print('Note: regardless of input filenames, the first image = frame 0.')
-    print('If your file names start from 0, adjust indexing accordingly for reading the output files.')
-    print(' ')
-    for hh in range(0, NtSlice):
-        print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
+    if rank == 0:
+        print('Note: regardless of input filenames, the first image = frame 0.')
+        print('If your file names start from 0, adjust indexing accordingly for reading the output files.')
+        print(' ')
+        for hh in range(0, NtSlice):
+            print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
 
     prefix = str(savedir / imNameSave)
     names = ('vx', 'vy', 'vz', 'rel') if spatialDimensions == 3 else ('vx', 'vy', 'rel')
     flow = calc_flow3D if spatialDimensions == 3 else calc_flow2D
 
     if fileType == 'OneTif':
-        allImages = tf.memmap(imDir / (imName + '.tif'))
+        try:
+            allImages = tf.memmap(imDir / (imName + '.tif'))
+        except ValueError:  # compressed / tiled / scattered pages: decoded into memory
+            allImages = tf.imread(imDir / (imName + '.tif'))
         load_frame = lambda i: allImages[i]
+        load_planes = lambda i, z0, z1: np.asarray(allImages[i][z0:z1])
     else:
         load_frame = lambda i: tf.imread(imDir / fileList[i])
+        load_planes = lambda i, z0, z1: tf.TiffFile(imDir / fileList[i]).read_planes(z0, z1)
     nOut = int(Nt) - NtChunk + 1
     rt = math.ceil(3 * tSig)
     if precision not in ("fp64", "fp32"):
         raise ValueError("precision must be 'fp64' or 'fp32'")
     if matlab_output and precision != "fp64":
         raise ValueError("matlab_output writes float64 files: use precision='fp64'")
+    if parallel not in ("auto", "frames", "zslab"):
+        raise ValueError("parallel must be 'auto', 'frames' or 'zslab'")
     writer = tf.imwrite_matlab if matlab_output else None
-    if nOut > 0 and NtChunk == 2 * rt + 1:
-        _process_stream(load_frame, nOut, NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix, names,
-                        precision, writer)
-    else:  # window and temporal taps disagree (non-integer 6*tSig+1): one upload per window
-        for hh in range(0, nOut):
-            loopStart = datetime.now()
-            print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
-            images = np.stack([load_frame(hh + jj) for jj in range(NtChunk)])
-            if matlab_output and spatialDimensions == 3:
-                out = _flow3d(images, xyzSig, tSig, wSig, rel_fp64=True)
-            elif precision == "fp64":
-                out = flow(images, xyzSig, tSig, wSig)
-            else:
-                out = _flow_fp32(images, spatialDimensions, xyzSig, tSig, wSig)
-            _write_frame(prefix, names, hh + NtSlice, out, writer=writer)
-            del out, images
-            print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(datetime.now() - loopStart))
+    # multi-GPU split: z-slabs need the 3D ring path and uncompressed (slab-writable) outputs
+    zslab_ok = world > 1 and spatialDimensions == 3 and not matlab_output and NtChunk == 2 * rt + 1 and nOut > 0
+    use_zslab = zslab_ok and (parallel == "zslab" or (parallel == "auto" and nOut < world))
+    if use_zslab:
+        _process_zslab(load_planes, Nz, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, prefix, names, precision,
+                       rank, world)
+    else:
+        from .shard import frame_blocks
 
-    for hh in range(int(Nt) - NtSlice, int(Nt)):
-        print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
+        h0, h1 = frame_blocks(nOut, rank, world) if nOut > 0 else (0, 0)
+        if h1 > h0 and NtChunk == 2 * rt + 1:
+            _process_stream(load_frame, (h0, h1), NtChunk, NtSlice, spatialDimensions, xyzSig, tSig, wSig, prefix,
+                            names, precision, writer)
+        else:  # window and temporal taps disagree (non-integer 6*tSig+1): one upload per window
+            for hh in range(h0, h1):
+                loopStart = datetime.now()
+                print(_now() + ' - Processing frame ' + str(hh + NtSlice) + '...')
+                images = np.stack([load_frame(hh + jj) for jj in range(NtChunk)])
+                if matlab_output and spatialDimensions == 3:
+                    out = _flow3d(images, xyzSig, tSig, wSig, rel_fp64=True)
+                elif precision == "fp64":
+                    out = flow(images, xyzSig, tSig, wSig)
+                else:
+                    out = _flow_fp32(images, spatialDimensions, xyzSig, tSig, wSig)
+                _write_frame(prefix, names, hh + NtSlice, out, writer=writer)
+                del out, images
+                print(_now() + ' - Frame ' + str(hh + NtSlice) + ' saved.  Duration: ' + str(datetime.now() - loopStart))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()  # every rank's files (or planes of them) are written
+    if rank == 0:
+        for hh in range(int(Nt) - NtSlice, int(Nt)):
+            print(_now() + ' - No data will be saved for frame ' + str(hh) + ' to avoid edge effects')
 
 
 calc_flow = process_flow
@@ -305,17 +350,19 @@ class _Shape:
         self.shape = shape
 
 
-def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names, precision="fp64",
-                    write_fn=None):
+def _process_stream(load_frame, out_range, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig, prefix, names,
+                    precision="fp64", write_fn=None):
     """process_flow's loop on a device-resident frame ring (stream.py): one
     frame read + upload per output frame; compute, download and TIFF writing
     of consecutive frames overlap.  Files and stdout lines are the reference's
-    (both lines of a frame are printed once its files are written)."""
+    (both lines of a frame are printed once its files are written).
+    out_range = (h0, h1): the windows starting at frames h0 .. h1 - 1 (a rank's block)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from .stream import FlowStream, Writer
 
-    first = np.asarray(load_frame(0))
+    h0, h1 = out_range
+    first = np.asarray(load_frame(h0))
     if len((NtChunk,) + first.shape) != ndim + 1:
         print(_now() + ' - Processing frame ' + str(NtSlice) + '...')
         _check_args(_Shape((NtChunk,) + first.shape), ndim + 1, tSig, MSG_NDIM_3D if ndim == 3 else MSG_NDIM_2D)
@@ -335,13 +382,60 @@ def _process_stream(load_frame, nOut, NtChunk, NtSlice, ndim, xyzSig, tSig, wSig
     writer = Writer(finish)
     try:
         fs.push(first)
-        for i in range(1, NtChunk - 1):
+        for i in range(h0 + 1, h0 + NtChunk - 1):
             fs.push(load_frame(i))
-        for hh in range(nOut):
+        for hh in range(h0, h1):
             start = datetime.now()
             start_str = str(start)
             fs.push(load_frame(hh + NtChunk - 1))
             writer.put(hh + NtSlice, start, start_str, fs.submit())
+    finally:
+        writer.close()
+        pool.shutdown()
+        fs.close()
+
+
+def _process_zslab(load_planes, Nz, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, prefix, names, precision, rank,
+                   world):
+    """process_flow's loop on one z-slab rank: every frame's own planes [z0, z1) are read and
+    uploaded, the halo planes come from the z-neighbours (FlowStream(zslab=...), one frame's
+    halo per output frame), and the rank writes its planes of each output TIFF in place
+    (tiff.write_planes: the files end up byte-identical to single-GPU ones).  Rank 0 prints
+    the reference's per-frame lines once its own planes are written."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from .shard import zslab_bounds
+    from .stream import FlowStream, Writer
+
+    z0, z1 = zslab_bounds(Nz, rank, world)
+    first = np.asarray(load_planes(0, z0, z1))
+    Ny, Nx = first.shape[-2:]
+    dt = first.dtype.newbyteorder('=') if first.dtype.byteorder not in ('=', '|') else first.dtype
+    fs = FlowStream(3, (Nz, Ny, Nx), dt, xyzSig, tSig, wSig, precision=precision, zslab=(rank, world, None))
+
+    def finish(frame, start, start_str, pending):
+        try:
+            out = pending.result()
+            tstr = str(frame).zfill(4)
+            for f in [pool.submit(tf.write_planes, prefix + '_' + n + '_t' + tstr + '.tiff', (Nz, Ny, Nx), a.dtype,
+                                  z0, a) for n, a in zip(names, out)]:
+                f.result()
+        finally:
+            pending.release()
+        if rank == 0:
+            print(start_str + ' - Processing frame ' + str(frame) + '...')
+            print(_now() + ' - Frame ' + str(frame) + ' saved.  Duration: ' + str(datetime.now() - start))
+
+    pool = ThreadPoolExecutor(len(names))
+    writer = Writer(finish)
+    try:
+        fs.push(first)
+        for i in range(1, NtChunk - 1):
+            fs.push(load_planes(i, z0, z1))
+        for hh in range(nOut):
+            start = datetime.now()
+            fs.push(load_planes(hh + NtChunk - 1, z0, z1))
+            writer.put(hh + NtSlice, start, str(start), fs.submit())
     finally:
         writer.close()
         pool.shutdown()

@@ -1,6 +1,6 @@
 """Multi-GPU decomposition of the LK hot path.
 
-Two ways the path shards, both one process per GPU:
+Two ways the path shards, both one process per GPU (process_flow picks one per run):
 
 1. Frame replicas — output frames are independent (the reference's own note,
    calc_flow.py:512: "this could become a parfor loop").  Rank r takes output
@@ -26,9 +26,99 @@ from . import _lib
 from .taps import make_taps, radii
 
 
+def init_distributed(backend=None):
+    """One process per GPU under torchrun (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* in the
+    environment): selects GPU LOCAL_RANK and initialises torch.distributed — RCCL ("nccl")
+    by default, $OF3D_DIST_BACKEND or `backend` to override (gloo: tests / rehearsals).
+    Returns (rank, world).  process_flow then splits its work over the ranks."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world == 1 or dist.is_initialized():
+        return (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+    backend = backend or os.environ.get("OF3D_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ngpu = torch.cuda.device_count()
+    gpu = local % max(ngpu, 1)
+    os.environ["OF3D_DEVICE"] = str(gpu)
+    if ngpu:
+        torch.cuda.set_device(gpu)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    else:
+        dist.init_process_group(backend)
+    return rank, world
+
+
 def frame_assignment(n_frames: int, rank: int, world: int) -> list:
     """Output frames of rank `rank` under round-robin replicas."""
     return list(range(rank, n_frames, world))
+
+
+def frame_blocks(n_frames: int, rank: int, world: int) -> tuple:
+    """Contiguous output frames [a, b) of rank `rank` (balanced): a rank streaming its block
+    through a frame ring uploads b - a + 2 rt frames instead of (b - a) (2 rt + 1)."""
+    return zslab_bounds(n_frames, rank, world)
+
+
+def halo_transfers(nz: int, rank: int, world: int, halo: int) -> tuple:
+    """One frame's halo traffic of rank `rank`: ([(peer, s0, s1)] planes it sends,
+    [(peer, g0, g1)] planes it receives); global plane indices.  Slabs thinner than the
+    halo exchange with several ranks; empty slabs neither send nor receive."""
+    z0, z1 = zslab_bounds(nz, rank, world)
+    if z1 <= z0:
+        return [], []
+    zi0, zi1 = max(z0 - halo, 0), min(z1 + halo, nz)
+    sends, recvs = [], []
+    for r in range(world):
+        rz0, rz1 = zslab_bounds(nz, r, world)
+        if r == rank or rz1 <= rz0:
+            continue
+        s0, s1 = max(max(rz0 - halo, 0), z0), min(min(rz1 + halo, nz), z1)
+        if s1 > s0:
+            sends.append((r, s0, s1))
+        g0, g1 = max(zi0, rz0), min(zi1, rz1)
+        if g1 > g0:
+            recvs.append((r, g0, g1))
+    return sends, recvs
+
+
+def exchange_frame_halo(block, zi0: int, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
+    """Halo exchange of ONE frame of a z-slab time series (the per-step traffic of
+    FlowStream(zslab=...)): ``block`` (zi1 - zi0, ny, nx) holds this rank's planes
+    [z0, z1) at offset z0 - zi0; the neighbours' planes are received straight into it and
+    this rank's boundary planes sent from it (whole planes are contiguous: no staging on
+    RCCL).  CUDA tensors over RCCL run on the current stream (the caller's upload stream,
+    so the exchange overlaps compute on another stream); gloo stages through host memory.
+    Every rank calls it for the same frames in the same order."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1 or block is None:
+        return
+    sends, recvs = halo_transfers(nz, rank, world, halo)
+    if not sends and not recvs:
+        return
+    stage = block.is_cuda and dist.get_backend(group) == "gloo"
+    ops, back = [], []
+    for peer, a, b in sends:
+        t = block[a - zi0:b - zi0]
+        ops.append(dist.P2POp(dist.isend, _bytes(t.cpu() if stage else t), peer, group))
+    for peer, a, b in recvs:
+        t = block[a - zi0:b - zi0]
+        if stage:
+            buf = torch.empty(t.shape, dtype=t.dtype)
+            back.append((t, buf))
+            t = buf
+        ops.append(dist.P2POp(dist.irecv, _bytes(t), peer, group))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+    for t, buf in back:
+        t.copy_(buf)
 
 
 def zslab_bounds(nz: int, rank: int, world: int) -> tuple:

@@ -47,8 +47,16 @@ class FlowStream:
     .release() hands the buffer set back (at most `depth` frames in flight)."""
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
-                 d2h_blocks=64, precision="fp64", rel_fp64=False):
+                 d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None):
+        """zslab=(rank, world, group): this process holds output planes
+        shard.zslab_bounds(nz, rank, world) of every frame (3D only).  push() then takes
+        the rank's own planes (z1 - z0, ny, nx) and fetches the frame's rd + rw halo planes
+        from the z-neighbours (torch.distributed P2P: RCCL over xGMI, or gloo) on the upload
+        stream — one frame's halo per output frame, overlapped with the previous frame's
+        compute; results are the rank's planes of vx, vy, vz, rel (no gather)."""
         import torch
+
+        from .shard import halo_planes, zslab_bounds
 
         self.torch = torch
         self.ndim = ndim
@@ -64,20 +72,34 @@ class FlowStream:
             nz, ny, nx = vol_shape
         else:
             (ny, nx), nz = vol_shape, 1
-        self.shape = tuple(vol_shape)
-        self.nvox = nz * ny * nx
+        self.nz, self.ny, self.nx = nz, ny, nx
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.nwin = 2 * self.rt + 1
+        if zslab is not None and ndim != 3:
+            raise ValueError("z-slabs need a 3D volume")
+        self.rank, self.world, self.group = zslab if zslab is not None else (0, 1, None)
+        self.z0, self.z1 = zslab_bounds(nz, self.rank, self.world)
+        self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw) if zslab is not None else (0, nz)
+        plane = ny * nx
+        self.shape = tuple(vol_shape) if zslab is None else (self.z1 - self.z0, ny, nx)  # pushed / returned
+        self.nvox = (self.z1 - self.z0) * plane
+        self.nblock = (self.zi1 - self.zi0) * plane
+        self.own0 = (self.z0 - self.zi0) * plane  # own planes' offset in a ring slot
         if precision not in ("fp64", "fp32"):
             raise ValueError("precision must be 'fp64' (bit-exact) or 'fp32'")
         self.precision = precision
         mode = (_lib.OF3D_FP32 if precision == "fp32" else 0) | (_lib.OF3D_REL_F64 if rel_fp64 else 0)
-        self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device, mode=mode)
-        self.ring = torch.empty((self.nwin, self.nvox), dtype=tdt, device=self.dev)
+        self.plan = None
+        if self.nvox > 0:
+            self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device, mode=mode,
+                                  max_out_planes=self.z1 - self.z0 if zslab is not None else 0)
+            if zslab is not None:
+                assert self.plan.input_range(self.z0, self.z1) == (self.zi0, self.zi1)
+        self.ring = torch.empty((self.nwin, max(self.nblock, 1)), dtype=tdt, device=self.dev)
         self.order = []  # ring slots of the resident frames, oldest first
         self.free = list(range(self.nwin))
-        self.stage = [torch.empty(self.nvox, dtype=tdt).pin_memory() for _ in range(2)]
-        self.stage_np = [t.numpy().view(dt).reshape(self.shape) for t in self.stage]
+        self.stage = [torch.empty(max(self.nvox, 1), dtype=tdt).pin_memory() for _ in range(2)]
+        self.stage_np = [t.numpy().view(dt)[:self.nvox].reshape(self.shape) for t in self.stage]
         self.stage_evt = [None, None]
         self.stage_i = 0
         # Downloads (d2h):
@@ -111,9 +133,10 @@ class FlowStream:
             rel_t = torch.float64 if (ndim == 2 or rel_fp64) else torch.float32
         self.depth = depth
         self.d2h_blocks = d2h_blocks
-        mk = lambda pin: [torch.empty(self.nvox, dtype=v_t, device=None if pin else self.dev,
+        nv = max(self.nvox, 1)
+        mk = lambda pin: [torch.empty(nv, dtype=v_t, device=None if pin else self.dev,
                                       pin_memory=pin) for _ in range(nout - 1)] + \
-                         [torch.empty(self.nvox, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
+                         [torch.empty(nv, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
         self.dout = [mk(False) for _ in range(depth)]
         self.hout = [mk(True) for _ in range(depth)]
         self.host_free = [threading.Event() for _ in range(depth)]  # set: writer released the set
@@ -138,12 +161,25 @@ class FlowStream:
         with torch.cuda.stream(self.h2d):
             if slot in self.slot_evt:
                 self.h2d.wait_event(self.slot_evt[slot])  # no compute still reads this slot
-            self.ring[slot].copy_(st, non_blocking=True)
+            if self.nvox:
+                self.ring[slot, self.own0:self.own0 + self.nvox].copy_(st[:self.nvox], non_blocking=True)
+            if self.world > 1:  # this frame's halo planes from / to the z-neighbours
+                self.exchange(slot)
             ev = torch.cuda.Event()
             ev.record(self.h2d)
         self.stage_evt[self.stage_i] = ev
         self.stage_i ^= 1
         self.order.append(slot)
+
+    def exchange(self, slot):
+        """Halo planes of the frame in ring slot `slot` (z-slab streams): issued on the current
+        stream (the upload stream in push); every rank calls it for the same frame."""
+        from .shard import exchange_frame_halo
+
+        blk = self.ring[slot, :max(self.nblock, 1)]
+        exchange_frame_halo(blk[:self.nblock].view(self.zi1 - self.zi0, self.ny, self.nx) if self.nblock else None,
+                            self.zi0, self.z0, self.z1, self.nz, self.rd + self.rw, self.rank, self.world,
+                            self.group)
 
     @property
     def ready(self):
@@ -160,8 +196,9 @@ class FlowStream:
         self.comp.wait_stream(self.h2d)
         ptrs = [self.ring[s].data_ptr() for s in self.order]
         vz = dout[2].data_ptr() if self.ndim == 3 else 0
-        self.plan.execute(ptrs, self.code, 0, 0, self.shape[0] if self.ndim == 3 else 1,
-                          dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
+        if self.plan is not None:
+            self.plan.execute(ptrs, self.code, self.zi0, self.z0, self.z1 if self.ndim == 3 else 1,
+                              dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
         cev = torch.cuda.Event()
         cev.record(self.comp)
         for s in self.order:
@@ -192,8 +229,9 @@ class FlowStream:
                 t0 = time.perf_counter()
                 cev.synchronize()
                 t1 = time.perf_counter()
-                _lib.dma_copy([h.data_ptr() for h in hout], [d.data_ptr() for d in dout],
-                              [d.numel() * d.element_size() for d in dout])
+                if self.nvox:
+                    _lib.dma_copy([h.data_ptr() for h in hout], [d.data_ptr() for d in dout],
+                                  [d.numel() * d.element_size() for d in dout])
                 t2 = time.perf_counter()
                 self.stats["dl_wait_s"] += t1 - t0
                 self.stats["dl_copy_s"] += t2 - t1
@@ -210,7 +248,8 @@ class FlowStream:
             self.dl_thread.join()
             self.dl_q = None
         self.torch.cuda.synchronize(self.dev)
-        self.plan.close()
+        if self.plan is not None:
+            self.plan.close()
 
 
 class Pending:
@@ -228,8 +267,8 @@ class Pending:
             self.done.wait()
             if self.error is not None:
                 raise self.error
-        shp = self.fs.shape
-        return [t.numpy().reshape(shp) for t in self.fs.hout[self.b]]
+        shp, n = self.fs.shape, self.fs.nvox
+        return [t.numpy()[:n].reshape(shp) for t in self.fs.hout[self.b]]
 
     def release(self):
         self.fs.host_free[self.b].set()

@@ -222,10 +222,37 @@ class TiffFile:
             raise ValueError(f"{self.path}: image data is not contiguous; cannot memory-map")
         return np.memmap(self.path, dtype=self.pages[0].dtype, mode="r", offset=blk[0], shape=self.series_shape())
 
+    def _needs_codec(self):
+        """Compressed or tiled pages: decoded through the system libtiff."""
+        return any(p.compression != 1 or not p.offsets for p in self.pages)
+
+    def read_planes(self, z0, z1):
+        """Pages [z0, z1) of a plain page series (a SequenceT time point), as (z1 - z0, y, x):
+        only those bytes are read when the pages are uncompressed."""
+        p0 = self.pages[0]
+        if self._needs_codec():
+            return np.ascontiguousarray(imread_libtiff(self.path).reshape((len(self.pages),) + p0.shape)[z0:z1])
+        blk = self._contiguous_block()
+        out = np.empty((z1 - z0,) + p0.shape, p0.dtype.newbyteorder("="))
+        with open(self.path, "rb") as f:
+            if blk is not None:
+                f.seek(blk[0] + z0 * p0.nbytes)
+                out[...] = np.frombuffer(f.read((z1 - z0) * p0.nbytes), dtype=p0.dtype).reshape(out.shape)
+                return out
+            for k, p in enumerate(self.pages[z0:z1]):
+                chunks = []
+                for o, c in zip(p.offsets, p.counts):
+                    f.seek(o)
+                    chunks.append(f.read(c))
+                out[k] = np.frombuffer(b"".join(chunks), dtype=p.dtype)[: int(np.prod(p.shape))].reshape(p.shape)
+        return out
+
     def asarray(self):
         blk = self._contiguous_block()
         shape = self.series_shape()
         p0 = self.pages[0]
+        if self._needs_codec():  # LZW / deflate / tiled inputs (tifffile decodes them too)
+            return np.ascontiguousarray(imread_libtiff(self.path).reshape(shape), dtype=p0.dtype.newbyteorder("="))
         if blk is not None:
             with open(self.path, "rb") as f:
                 f.seek(blk[0])
@@ -274,17 +301,51 @@ def imwrite(path, data, photometric="minisblack", description=None, imagej=False
     if arr.dtype.kind == "b":
         arr = arr.astype(np.uint8)
     arr = np.ascontiguousarray(arr, dtype=arr.dtype.newbyteorder("<"))
-    if arr.ndim < 2:
-        arr = arr.reshape((1,) * (2 - arr.ndim) + arr.shape)
-    ny, nx = arr.shape[-2:]
-    npages = int(np.prod(arr.shape[:-2])) if arr.ndim > 2 else 1
-    fmt = {"u": 1, "i": 2, "f": 3}[arr.dtype.kind]
-    bits = arr.dtype.itemsize * 8
+    head, data_pos, tail = _layout(arr.shape, arr.dtype, description, imagej, bigtiff)
+    flat = arr.reshape(-1)
+    with open(path, "wb") as f:
+        f.write(head)
+        f.write(memoryview(flat).cast("B"))
+        f.write(tail)
+
+
+def write_planes(path, shape, dtype, z0, planes, description=None, imagej=False, bigtiff=None):
+    """Write planes [z0, z0 + len(planes)) of a TIFF whose full content is ``imwrite(path,
+    full_array)`` for a ``shape`` / ``dtype`` array (several processes each writing their
+    own z-slab of one output volume; no gather, no coordination: every writer puts the
+    same header and trailing IFDs in place and sizes the file, the planes are disjoint).
+    Once every plane has been written, the file is byte-identical to imwrite's."""
+    dt = np.dtype(dtype).newbyteorder("<")
+    head, data_pos, tail = _layout(tuple(shape), dt, description, imagej, bigtiff)
+    plane_bytes = int(shape[-1]) * int(shape[-2]) * dt.itemsize
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    arr = np.ascontiguousarray(planes, dtype=dt)
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)
+    try:
+        os.ftruncate(fd, data_pos + nbytes + len(tail))
+        os.pwrite(fd, head, 0)
+        os.pwrite(fd, tail, data_pos + nbytes)
+        if arr.size:
+            os.pwrite(fd, memoryview(arr.reshape(-1)).cast("B"), data_pos + int(z0) * plane_bytes)
+    finally:
+        os.close(fd)
+
+
+def _layout(shape, dtype, description=None, imagej=False, bigtiff=None):
+    """(header + first IFD bytes, data offset, trailing IFD bytes) of imwrite's file for an
+    array of ``shape`` / little-endian ``dtype``."""
+    dtype = np.dtype(dtype)
+    if len(shape) < 2:
+        shape = (1,) * (2 - len(shape)) + tuple(shape)
+    ny, nx = shape[-2:]
+    npages = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    fmt = {"u": 1, "i": 2, "f": 3}[dtype.kind]
+    bits = dtype.itemsize * 8
     if description is None:
-        description = imagej_description(arr.shape) if imagej else json.dumps({"shape": list(arr.shape)})
+        description = imagej_description(shape) if imagej else json.dumps({"shape": list(shape)})
     desc = description.encode("latin-1") + b"\0"
     software = b"opticalflow3d_dev_amd\0"
-    plane_bytes = ny * nx * arr.dtype.itemsize
+    plane_bytes = ny * nx * dtype.itemsize
     if bigtiff is None:
         bigtiff = npages * (plane_bytes + 320) + len(desc) + 64 > _BIGTIFF_THRESHOLD
     ofmt, osz = ("Q", 8) if bigtiff else ("I", 4)
@@ -326,13 +387,13 @@ def imwrite(path, data, photometric="minisblack", description=None, imagej=False
     _, blk0 = ifd_block(0, ifd0_pos, 0)
     data_pos = ifd0_pos + len(blk0)
     data_pos += (-data_pos) % 16
-    flat = arr.reshape(-1)
+    nbytes = npages * plane_bytes
     body0, blk0 = ifd_block(0, ifd0_pos, data_pos)
     head = bytearray(header + blk0)
     head += b"\0" * (data_pos - len(head))
     # IFDs of pages 1.. assembled in memory (next-IFD links patched there), one write
     tail = bytearray()
-    base = data_pos + flat.nbytes
+    base = data_pos + nbytes
     prev = (head, ifd0_pos + len(body0))  # (buffer, offset of the next-IFD field in it)
     for i in range(1, npages):
         if (base + len(tail)) & 1:
@@ -343,10 +404,7 @@ def imwrite(path, data, photometric="minisblack", description=None, imagej=False
         buf[at:at + osz] = struct.pack("<" + ofmt, pos)
         prev = (tail, len(tail) + len(body))
         tail += blk
-    with open(path, "wb") as f:
-        f.write(head)
-        f.write(memoryview(flat).cast("B"))
-        f.write(tail)
+    return bytes(head), data_pos, bytes(tail)
 
 
 def imagej_description(shape, frames=None, slices=None):
@@ -383,7 +441,8 @@ def natsorted(items):
 # same library writes them here, through ctypes on the system libtiff.
 # ---------------------------------------------------------------------------
 _TIFFTAG = dict(IMAGEWIDTH=256, IMAGELENGTH=257, BITSPERSAMPLE=258, COMPRESSION=259, PHOTOMETRIC=262,
-                SAMPLESPERPIXEL=277, ROWSPERSTRIP=278, PLANARCONFIG=284, SAMPLEFORMAT=339)
+                SAMPLESPERPIXEL=277, ROWSPERSTRIP=278, PLANARCONFIG=284, SAMPLEFORMAT=339, TILEWIDTH=322,
+                TILELENGTH=323)
 _libtiff_handle = None
 
 
@@ -419,6 +478,14 @@ def _libtiff():
         lib.TIFFReadDirectory.restype = ctypes.c_int
         lib.TIFFClose.argtypes = [P]
         lib.TIFFClose.restype = None
+        lib.TIFFIsTiled.argtypes = [P]
+        lib.TIFFIsTiled.restype = ctypes.c_int
+        lib.TIFFComputeTile.argtypes = [P, U32, U32, U32, ctypes.c_uint16]
+        lib.TIFFComputeTile.restype = U32
+        lib.TIFFReadEncodedTile.argtypes = [P, U32, P, ctypes.c_int64]
+        lib.TIFFReadEncodedTile.restype = ctypes.c_int64
+        lib.TIFFWriteEncodedTile.argtypes = [P, U32, P, ctypes.c_int64]
+        lib.TIFFWriteEncodedTile.restype = ctypes.c_int64
         _libtiff_handle = lib
     return _libtiff_handle
 
@@ -429,19 +496,27 @@ def imwrite_matlab(path, data):
     MATLAB mode), MinIsBlack, chunky, LZW, libtiff's default strip size.
     The encoding runs in libtiff with the GIL released (ctypes), so several
     files can be written from threads at once."""
+    if np.asarray(data).dtype.kind != "f":
+        raise ValueError("MATLAB-mode outputs are floating point")
+    imwrite_libtiff(path, data, compression=5, bigtiff=True)
+
+
+def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, tile=None):
+    """One page per plane through the system libtiff: ``compression`` (5 LZW, 8 deflate,
+    1 none), optional ImageDescription, strips of libtiff's default size or ``tile``
+    (th, tw) tiles (multiples of 16).  Integer or float samples."""
     import ctypes
 
     lib = _libtiff()
     arr = np.asarray(data)
-    if arr.dtype.kind != "f":
-        raise ValueError("MATLAB-mode outputs are floating point")
     arr = np.ascontiguousarray(arr, dtype=arr.dtype.newbyteorder("="))
     if arr.ndim == 2:
         arr = arr[None]
     if arr.ndim != 3:
         raise ValueError("expected a 2-D image or a (z, y, x) volume")
     nz, ny, nx = arr.shape
-    tif = lib.TIFFOpen(os.fsencode(str(path)), b"w8")
+    fmt = {"u": 1, "i": 2, "f": 3}[arr.dtype.kind]
+    tif = lib.TIFFOpen(os.fsencode(str(path)), b"w8" if bigtiff else b"w")
     if not tif:
         raise OSError("libtiff could not create " + str(path))
     U32, I = ctypes.c_uint32, ctypes.c_int
@@ -450,17 +525,34 @@ def imwrite_matlab(path, data):
         for z in range(nz):
             for tag, val in ((T["IMAGELENGTH"], U32(ny)), (T["IMAGEWIDTH"], U32(nx)), (T["SAMPLESPERPIXEL"], I(1)),
                              (T["PLANARCONFIG"], I(1)), (T["BITSPERSAMPLE"], I(8 * arr.itemsize)),
-                             (T["SAMPLEFORMAT"], I(3)), (T["PHOTOMETRIC"], I(1)), (T["COMPRESSION"], I(5))):
+                             (T["SAMPLEFORMAT"], I(fmt)), (T["PHOTOMETRIC"], I(1)),
+                             (T["COMPRESSION"], I(compression))):
                 if not lib.TIFFSetField(ctypes.c_void_p(tif), U32(tag), val):
                     raise OSError("libtiff rejected tag %d" % tag)
-            rps = int(lib.TIFFDefaultStripSize(tif, 0))
-            lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["ROWSPERSTRIP"]), U32(rps))
+            if description is not None and z == 0:
+                lib.TIFFSetField(ctypes.c_void_p(tif), U32(270), ctypes.c_char_p(description.encode("latin-1")))
             plane = arr[z]
-            row_bytes = nx * arr.itemsize
-            for s, r0 in enumerate(range(0, ny, rps)):
-                chunk = plane[r0:r0 + rps]
-                if lib.TIFFWriteEncodedStrip(tif, s, chunk.ctypes.data, chunk.shape[0] * row_bytes) < 0:
-                    raise OSError("libtiff failed writing " + str(path))
+            if tile is None:
+                rps = int(lib.TIFFDefaultStripSize(tif, 0))
+                lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["ROWSPERSTRIP"]), U32(rps))
+                row_bytes = nx * arr.itemsize
+                for s, r0 in enumerate(range(0, ny, rps)):
+                    chunk = plane[r0:r0 + rps]
+                    if lib.TIFFWriteEncodedStrip(tif, s, chunk.ctypes.data, chunk.shape[0] * row_bytes) < 0:
+                        raise OSError("libtiff failed writing " + str(path))
+            else:
+                th, tw = tile
+                lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["TILEWIDTH"]), U32(tw))
+                lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["TILELENGTH"]), U32(th))
+                buf = np.zeros((th, tw), arr.dtype)
+                for ty in range(0, ny, th):
+                    for tx in range(0, nx, tw):
+                        buf[...] = 0
+                        blk = plane[ty:ty + th, tx:tx + tw]
+                        buf[:blk.shape[0], :blk.shape[1]] = blk
+                        if lib.TIFFWriteEncodedTile(tif, lib.TIFFComputeTile(tif, tx, ty, 0, 0), buf.ctypes.data,
+                                                    buf.nbytes) < 0:
+                            raise OSError("libtiff failed writing " + str(path))
             if not lib.TIFFWriteDirectory(tif):
                 raise OSError("libtiff failed writing " + str(path))
     finally:
@@ -488,11 +580,22 @@ def imread_libtiff(path):
             out = np.empty((h, w), dt)
             buf = out.reshape(-1).view(np.uint8)
             pos = 0
-            for s in range(lib.TIFFNumberOfStrips(tif)):
+            for s in range(0 if lib.TIFFIsTiled(tif) else lib.TIFFNumberOfStrips(tif)):
                 n = lib.TIFFReadEncodedStrip(tif, s, buf[pos:].ctypes.data, buf.size - pos)
                 if n < 0:
                     raise OSError("libtiff failed decoding " + str(path))
                 pos += n
+            buf = out.reshape(-1).view(np.uint8)
+            if lib.TIFFIsTiled(tif):
+                tw, th = get(T["TILEWIDTH"], ctypes.c_uint32), get(T["TILELENGTH"], ctypes.c_uint32)
+                tile = np.empty((th, tw), dt)
+                for ty in range(0, h, th):
+                    for tx in range(0, w, tw):
+                        n = lib.TIFFReadEncodedTile(tif, lib.TIFFComputeTile(tif, tx, ty, 0, 0), tile.ctypes.data,
+                                                    tile.nbytes)
+                        if n < 0:
+                            raise OSError("libtiff failed decoding " + str(path))
+                        out[ty:ty + th, tx:tx + tw] = tile[:min(th, h - ty), :min(tw, w - tx)]
             pages.append(out)
             if not lib.TIFFReadDirectory(tif):
                 break
