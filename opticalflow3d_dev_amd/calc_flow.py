@@ -200,9 +200,11 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     rank streams a contiguous block of output frames and writes their files;
     ``parallel="zslab"`` (3D): every rank reads only its z-planes of each frame, fetches
     the stencil halo planes from its z-neighbours (RCCL P2P) and writes its planes of
-    every output file (shard, tiff.write_planes; no gather).  ``"auto"``: frames when
-    there are at least as many output frames as ranks, else z-slabs.  Files and pixel
-    values are the same as on one GPU."""
+    every output file (shard, tiff.write_planes; no gather); ``"yslab"``: the same with
+    rows of every plane (less halo work when Ny >> Nz: the y pass is the first pass of
+    both filter chains).  ``"auto"``: frames when there are at least as many output
+    frames as ranks, else the slab axis with less predicted halo work
+    (shard.slab_axis).  Files and pixel values are the same as on one GPU."""
     ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
     imDir = Path(imDir)
     if not imDir.is_dir():
@@ -289,15 +291,27 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
         raise ValueError("precision must be 'fp64' or 'fp32'")
     if matlab_output and precision != "fp64":
         raise ValueError("matlab_output writes float64 files: use precision='fp64'")
-    if parallel not in ("auto", "frames", "zslab"):
-        raise ValueError("parallel must be 'auto', 'frames' or 'zslab'")
+    if parallel not in ("auto", "frames", "zslab", "yslab"):
+        raise ValueError("parallel must be 'auto', 'frames', 'zslab' or 'yslab'")
     writer = tf.imwrite_matlab if matlab_output else None
-    # multi-GPU split: z-slabs need the 3D ring path and uncompressed (slab-writable) outputs
-    zslab_ok = world > 1 and spatialDimensions == 3 and not matlab_output and NtChunk == 2 * rt + 1 and nOut > 0
-    use_zslab = zslab_ok and (parallel == "zslab" or (parallel == "auto" and nOut < world))
-    if use_zslab:
-        _process_zslab(load_planes, Nz, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, prefix, names, precision,
-                       rank, world)
+    # multi-GPU split: slabs need the 3D ring path and uncompressed (slab-writable) outputs
+    slab_ok = world > 1 and spatialDimensions == 3 and not matlab_output and NtChunk == 2 * rt + 1 and nOut > 0
+    axis = None
+    if slab_ok and parallel in ("zslab", "yslab"):
+        axis = 0 if parallel == "zslab" else 1
+    elif slab_ok and parallel == "auto" and nOut < world:
+        from .shard import slab_axis
+        from .taps import radii
+
+        rd_, _, _, rw_ = radii(xyzSig, tSig, wSig)
+        axis = slab_axis(int(Nz), int(Ny), world, rd_, rw_)
+    if axis is not None:
+        if fileType == 'OneTif':
+            load_rows = lambda i, y0, y1: np.asarray(allImages[i][:, y0:y1])
+        else:
+            load_rows = lambda i, y0, y1: tf.TiffFile(imDir / fileList[i]).read_rows(y0, y1)
+        _process_slab(load_planes if axis == 0 else load_rows, axis, (int(Nz), int(Ny), int(Nx)), nOut, NtChunk,
+                      NtSlice, xyzSig, tSig, wSig, prefix, names, precision, rank, world)
     else:
         from .shard import frame_blocks
 
@@ -395,30 +409,31 @@ def _process_stream(load_frame, out_range, NtChunk, NtSlice, ndim, xyzSig, tSig,
         fs.close()
 
 
-def _process_zslab(load_planes, Nz, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, prefix, names, precision, rank,
-                   world):
-    """process_flow's loop on one z-slab rank: every frame's own planes [z0, z1) are read and
-    uploaded, the halo planes come from the z-neighbours (FlowStream(zslab=...), one frame's
-    halo per output frame), and the rank writes its planes of each output TIFF in place
-    (tiff.write_planes: the files end up byte-identical to single-GPU ones).  Rank 0 prints
-    the reference's per-frame lines once its own planes are written."""
+def _process_slab(load_part, axis, vol, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, prefix, names, precision,
+                  rank, world):
+    """process_flow's loop on one slab rank (axis 0: z-planes, 1: rows): every frame's own part
+    is read and uploaded, the halo comes from the neighbours (FlowStream(zslab=...), one
+    frame's halo per output frame), and the rank writes its part of each output TIFF in place
+    (tiff.write_planes / write_rows: the files end up byte-identical to single-GPU ones).
+    Rank 0 prints the reference's per-frame lines once its own part is written."""
     from concurrent.futures import ThreadPoolExecutor
 
     from .shard import zslab_bounds
     from .stream import FlowStream, Writer
 
-    z0, z1 = zslab_bounds(Nz, rank, world)
-    first = np.asarray(load_planes(0, z0, z1))
-    Ny, Nx = first.shape[-2:]
+    Nz, Ny, Nx = vol
+    a0, a1 = zslab_bounds(vol[axis], rank, world)
+    first = np.asarray(load_part(0, a0, a1))
     dt = first.dtype.newbyteorder('=') if first.dtype.byteorder not in ('=', '|') else first.dtype
-    fs = FlowStream(3, (Nz, Ny, Nx), dt, xyzSig, tSig, wSig, precision=precision, zslab=(rank, world, None))
+    fs = FlowStream(3, vol, dt, xyzSig, tSig, wSig, precision=precision, zslab=(rank, world, None, axis))
+    write = tf.write_planes if axis == 0 else tf.write_rows
 
     def finish(frame, start, start_str, pending):
         try:
             out = pending.result()
             tstr = str(frame).zfill(4)
-            for f in [pool.submit(tf.write_planes, prefix + '_' + n + '_t' + tstr + '.tiff', (Nz, Ny, Nx), a.dtype,
-                                  z0, a) for n, a in zip(names, out)]:
+            for f in [pool.submit(write, prefix + '_' + n + '_t' + tstr + '.tiff', vol, a.dtype, a0, a)
+                      for n, a in zip(names, out)]:
                 f.result()
         finally:
             pending.release()
@@ -431,10 +446,10 @@ def _process_zslab(load_planes, Nz, nOut, NtChunk, NtSlice, xyzSig, tSig, wSig, 
     try:
         fs.push(first)
         for i in range(1, NtChunk - 1):
-            fs.push(load_planes(i, z0, z1))
+            fs.push(load_part(i, a0, a1))
         for hh in range(nOut):
             start = datetime.now()
-            fs.push(load_planes(hh + NtChunk - 1, z0, z1))
+            fs.push(load_part(hh + NtChunk - 1, a0, a1))
             writer.put(hh + NtSlice, start, str(start), fs.submit())
     finally:
         writer.close()

@@ -54,6 +54,29 @@ def init_distributed(backend=None):
     return rank, world
 
 
+# measured share of each stage in a c3 frame (profiles/r02c_c3_k12_bench.log): K0 tderiv,
+# K12 gradients, K34 products + W y + W x, K5c W z + solve
+STAGE_SHARE = {"tderiv": 0.08, "grad": 0.16, "prod_wyx": 0.49, "wz_solve": 0.27}
+
+
+def slab_work(n_split: int, n_other_split: int, world: int, rd: int, rw: int, axis: int) -> float:
+    """Predicted work of the busiest slab rank relative to 1/world of the frame, from the
+    stage shares: z-slabs (axis 0) recompute K0 / gradients on rd + rw and the products
+    on rw halo planes per cut side (K5c only on own planes); row slabs (axis 1) run the
+    whole pipeline on the rank's rows + rd + rw halo rows per cut side."""
+    own = -(-n_split // world)
+    cuts = 2 if world > 2 else (1 if world == 2 else 0)
+    if axis == 0:
+        extra = (STAGE_SHARE["tderiv"] + STAGE_SHARE["grad"]) * (rd + rw) + STAGE_SHARE["prod_wyx"] * rw
+        return 1.0 + cuts * extra / own
+    return 1.0 + cuts * (rd + rw) / own
+
+
+def slab_axis(nz: int, ny: int, world: int, rd: int, rw: int) -> int:
+    """The split axis with less predicted halo work: 0 (z-slabs) or 1 (row slabs)."""
+    return 0 if slab_work(nz, ny, world, rd, rw, 0) <= slab_work(ny, nz, world, rd, rw, 1) else 1
+
+
 def frame_assignment(n_frames: int, rank: int, world: int) -> list:
     """Output frames of rank `rank` under round-robin replicas."""
     return list(range(rank, n_frames, world))
@@ -94,7 +117,9 @@ def exchange_frame_halo(block, zi0: int, z0: int, z1: int, nz: int, halo: int, r
     this rank's boundary planes sent from it (whole planes are contiguous: no staging on
     RCCL).  CUDA tensors over RCCL run on the current stream (the caller's upload stream,
     so the exchange overlaps compute on another stream); gloo stages through host memory.
-    Every rank calls it for the same frames in the same order."""
+    Every rank calls it for the same frames in the same order.  ``block`` may be a strided
+    view whose first axis is the split axis (row slabs: rows first); non-contiguous pieces
+    travel through contiguous temporaries."""
     import torch
     import torch.distributed as dist
 
@@ -107,11 +132,12 @@ def exchange_frame_halo(block, zi0: int, z0: int, z1: int, nz: int, halo: int, r
     ops, back = [], []
     for peer, a, b in sends:
         t = block[a - zi0:b - zi0]
-        ops.append(dist.P2POp(dist.isend, _bytes(t.cpu() if stage else t), peer, group))
+        t = t.cpu() if stage else t.contiguous()
+        ops.append(dist.P2POp(dist.isend, _bytes(t), peer, group))
     for peer, a, b in recvs:
         t = block[a - zi0:b - zi0]
-        if stage:
-            buf = torch.empty(t.shape, dtype=t.dtype)
+        if stage or not t.is_contiguous():  # host staging (gloo) / strided rows (row slabs)
+            buf = torch.empty(t.shape, dtype=t.dtype, device="cpu" if stage else t.device)
             back.append((t, buf))
             t = buf
         ops.append(dist.P2POp(dist.irecv, _bytes(t), peer, group))

@@ -48,12 +48,16 @@ class FlowStream:
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
                  d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None):
-        """zslab=(rank, world, group): this process holds output planes
-        shard.zslab_bounds(nz, rank, world) of every frame (3D only).  push() then takes
-        the rank's own planes (z1 - z0, ny, nx) and fetches the frame's rd + rw halo planes
-        from the z-neighbours (torch.distributed P2P: RCCL over xGMI, or gloo) on the upload
-        stream — one frame's halo per output frame, overlapped with the previous frame's
-        compute; results are the rank's planes of vx, vy, vz, rel (no gather)."""
+        """zslab=(rank, world, group[, axis]): this process holds one slab of every frame (3D
+        only) — axis 0 (default): output planes shard.zslab_bounds(nz, rank, world); axis 1:
+        rows zslab_bounds(ny, rank, world) of every plane.  push() then takes the rank's own
+        part ((z1 - z0, ny, nx) or (nz, y1 - y0, nx)) and fetches the frame's rd + rw halo
+        planes / rows from its neighbours (torch.distributed P2P: RCCL over xGMI, or gloo) on
+        the upload stream — one frame's halo per output frame, overlapped with the previous
+        frame's compute; results are the rank's part of vx, vy, vz, rel (no gather).
+        Row slabs run the plan on the rank's rows + halo as a volume of its own (the y pass is
+        the first pass of both filter chains, so rows further than rd + rw from a cut are
+        exact: bit-identical), and keep the own rows."""
         import torch
 
         from .shard import halo_planes, zslab_bounds
@@ -77,27 +81,45 @@ class FlowStream:
         self.nwin = 2 * self.rt + 1
         if zslab is not None and ndim != 3:
             raise ValueError("z-slabs need a 3D volume")
-        self.rank, self.world, self.group = zslab if zslab is not None else (0, 1, None)
-        self.z0, self.z1 = zslab_bounds(nz, self.rank, self.world)
-        self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw) if zslab is not None else (0, nz)
+        self.rank, self.world, self.group = zslab[:3] if zslab is not None else (0, 1, None)
+        self.axis = zslab[3] if zslab is not None and len(zslab) > 3 else 0
         plane = ny * nx
-        self.shape = tuple(vol_shape) if zslab is None else (self.z1 - self.z0, ny, nx)  # pushed / returned
-        self.nvox = (self.z1 - self.z0) * plane
-        self.nblock = (self.zi1 - self.zi0) * plane
-        self.own0 = (self.z0 - self.zi0) * plane  # own planes' offset in a ring slot
+        taps = make_taps(xyzSig, tSig, wSig)
         if precision not in ("fp64", "fp32"):
             raise ValueError("precision must be 'fp64' (bit-exact) or 'fp32'")
         self.precision = precision
         mode = (_lib.OF3D_FP32 if precision == "fp32" else 0) | (_lib.OF3D_REL_F64 if rel_fp64 else 0)
         self.plan = None
-        if self.nvox > 0:
-            self.plan = _lib.Plan(ndim, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=self.device, mode=mode,
-                                  max_out_planes=self.z1 - self.z0 if zslab is not None else 0)
+        self.z0, self.z1, self.zi0, self.zi1 = 0, nz, 0, nz
+        self.y0, self.y1, self.yi0, self.yi1 = 0, ny, 0, ny
+        if self.axis == 0:
+            self.z0, self.z1 = zslab_bounds(nz, self.rank, self.world)
             if zslab is not None:
-                assert self.plan.input_range(self.z0, self.z1) == (self.zi0, self.zi1)
-        self.ring = torch.empty((self.nwin, max(self.nblock, 1)), dtype=tdt, device=self.dev)
+                self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw)
+            self.shape = tuple(vol_shape) if zslab is None else (self.z1 - self.z0, ny, nx)  # pushed / returned
+            self.nvox = (self.z1 - self.z0) * plane
+            self.nblock = (self.zi1 - self.zi0) * plane
+            self.own0 = (self.z0 - self.zi0) * plane  # own planes' offset in a ring slot
+            if self.nvox > 0:
+                self.plan = _lib.Plan(ndim, nz, ny, nx, taps, device=self.device, mode=mode,
+                                      max_out_planes=self.z1 - self.z0 if zslab is not None else 0)
+                if zslab is not None:
+                    assert self.plan.input_range(self.z0, self.z1) == (self.zi0, self.zi1)
+        else:
+            self.y0, self.y1 = zslab_bounds(ny, self.rank, self.world)
+            self.yi0, self.yi1 = halo_planes(ny, self.y0, self.y1, self.rd, self.rw)
+            self.shape = (nz, self.y1 - self.y0, nx)
+            self.nvox = nz * (self.y1 - self.y0) * nx
+            self.nblock = nz * (self.yi1 - self.yi0) * nx
+            self.own0 = 0
+            if self.nvox > 0:
+                self.plan = _lib.Plan(3, nz, self.yi1 - self.yi0, nx, taps, device=self.device, mode=mode)
+        # nwin + 1 slots: a new frame's upload (and halo exchange) goes to the slot the
+        # frame before last read, so it overlaps the previous frame's compute
+        self.ring = torch.empty((self.nwin + 1, max(self.nblock, 1)), dtype=tdt, device=self.dev)
         self.order = []  # ring slots of the resident frames, oldest first
-        self.free = list(range(self.nwin))
+        self.free = list(range(self.nwin + 1))
+        self.dstage = torch.empty(max(self.nvox, 1), dtype=tdt, device=self.dev) if self.axis == 1 else None
         self.stage = [torch.empty(max(self.nvox, 1), dtype=tdt).pin_memory() for _ in range(2)]
         self.stage_np = [t.numpy().view(dt)[:self.nvox].reshape(self.shape) for t in self.stage]
         self.stage_evt = [None, None]
@@ -134,11 +156,13 @@ class FlowStream:
         self.depth = depth
         self.d2h_blocks = d2h_blocks
         nv = max(self.nvox, 1)
-        mk = lambda pin: [torch.empty(nv, dtype=v_t, device=None if pin else self.dev,
-                                      pin_memory=pin) for _ in range(nout - 1)] + \
-                         [torch.empty(nv, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
+        mk = lambda pin, n=nv: [torch.empty(n, dtype=v_t, device=None if pin else self.dev,
+                                            pin_memory=pin) for _ in range(nout - 1)] + \
+                               [torch.empty(n, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
         self.dout = [mk(False) for _ in range(depth)]
         self.hout = [mk(True) for _ in range(depth)]
+        # row slabs: the plan writes all rows of its sub-volume here; the own rows are copied out
+        self.dfull = mk(False, max(self.nblock, 1)) if self.axis == 1 else None
         self.host_free = [threading.Event() for _ in range(depth)]  # set: writer released the set
         for e in self.host_free:
             e.set()
@@ -161,8 +185,12 @@ class FlowStream:
         with torch.cuda.stream(self.h2d):
             if slot in self.slot_evt:
                 self.h2d.wait_event(self.slot_evt[slot])  # no compute still reads this slot
-            if self.nvox:
+            if self.nvox and self.axis == 0:
                 self.ring[slot, self.own0:self.own0 + self.nvox].copy_(st[:self.nvox], non_blocking=True)
+            elif self.nvox:
+                self.dstage.copy_(st, non_blocking=True)
+                self._rows(self.ring[slot])[:, self.y0 - self.yi0:self.y1 - self.yi0].copy_(
+                    self.dstage[:self.nvox].view(self.shape))
             if self.world > 1:  # this frame's halo planes from / to the z-neighbours
                 self.exchange(slot)
             ev = torch.cuda.Event()
@@ -171,15 +199,24 @@ class FlowStream:
         self.stage_i ^= 1
         self.order.append(slot)
 
+    def _rows(self, flat):
+        """A ring slot / output buffer of a row-slab stream as (nz, yi1 - yi0, nx)."""
+        return flat[:self.nblock].view(self.nz, self.yi1 - self.yi0, self.nx)
+
     def exchange(self, slot):
-        """Halo planes of the frame in ring slot `slot` (z-slab streams): issued on the current
-        stream (the upload stream in push); every rank calls it for the same frame."""
+        """Halo planes (rows) of the frame in ring slot `slot` (slab streams): issued on the
+        current stream (the upload stream in push); every rank calls it for the same frame."""
         from .shard import exchange_frame_halo
 
-        blk = self.ring[slot, :max(self.nblock, 1)]
-        exchange_frame_halo(blk[:self.nblock].view(self.zi1 - self.zi0, self.ny, self.nx) if self.nblock else None,
-                            self.zi0, self.z0, self.z1, self.nz, self.rd + self.rw, self.rank, self.world,
-                            self.group)
+        if not self.nblock:
+            blk = None
+        elif self.axis == 0:
+            blk = self.ring[slot, :self.nblock].view(self.zi1 - self.zi0, self.ny, self.nx)
+        else:
+            blk = self._rows(self.ring[slot]).transpose(0, 1)  # rows first (strided)
+        lo, hi, i0, n = ((self.z0, self.z1, self.zi0, self.nz) if self.axis == 0 else
+                         (self.y0, self.y1, self.yi0, self.ny))
+        exchange_frame_halo(blk, i0, lo, hi, n, self.rd + self.rw, self.rank, self.world, self.group)
 
     @property
     def ready(self):
@@ -196,9 +233,16 @@ class FlowStream:
         self.comp.wait_stream(self.h2d)
         ptrs = [self.ring[s].data_ptr() for s in self.order]
         vz = dout[2].data_ptr() if self.ndim == 3 else 0
-        if self.plan is not None:
+        if self.plan is not None and self.axis == 0:
             self.plan.execute(ptrs, self.code, self.zi0, self.z0, self.z1 if self.ndim == 3 else 1,
                               dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
+        elif self.plan is not None:  # row slab: whole sub-volume, then the own rows
+            full = self.dfull
+            self.plan.execute(ptrs, self.code, 0, 0, self.nz, full[0].data_ptr(), full[1].data_ptr(),
+                              full[2].data_ptr(), full[3].data_ptr(), self.comp.cuda_stream)
+            with torch.cuda.stream(self.comp):
+                for d, f in zip(dout, full):
+                    d[:self.nvox].view(self.shape).copy_(self._rows(f)[:, self.y0 - self.yi0:self.y1 - self.yi0])
         cev = torch.cuda.Event()
         cev.record(self.comp)
         for s in self.order:

@@ -247,6 +247,15 @@ class TiffFile:
                 out[k] = np.frombuffer(b"".join(chunks), dtype=p.dtype)[: int(np.prod(p.shape))].reshape(p.shape)
         return out
 
+    def read_rows(self, y0, y1):
+        """Rows [y0, y1) of every page of a plain page series, as (pages, y1 - y0, x)."""
+        p0 = self.pages[0]
+        blk = self._contiguous_block()
+        if blk is not None and not self._needs_codec():
+            mm = np.memmap(self.path, dtype=p0.dtype, mode="r", offset=blk[0], shape=(len(self.pages),) + p0.shape)
+            return np.ascontiguousarray(mm[:, y0:y1], dtype=p0.dtype.newbyteorder("="))
+        return np.ascontiguousarray(self.read_planes(0, len(self.pages))[:, y0:y1])
+
     def asarray(self):
         blk = self._contiguous_block()
         shape = self.series_shape()
@@ -327,6 +336,29 @@ def write_planes(path, shape, dtype, z0, planes, description=None, imagej=False,
         os.pwrite(fd, tail, data_pos + nbytes)
         if arr.size:
             os.pwrite(fd, memoryview(arr.reshape(-1)).cast("B"), data_pos + int(z0) * plane_bytes)
+    finally:
+        os.close(fd)
+
+
+def write_rows(path, shape, dtype, y0, rows, description=None, imagej=False, bigtiff=None):
+    """write_planes for a row slab: rows [y0, y0 + rows.shape[-2]) of every plane of a
+    ``shape`` / ``dtype`` volume (several processes, disjoint rows, no coordination)."""
+    dt = np.dtype(dtype).newbyteorder("<")
+    head, data_pos, tail = _layout(tuple(shape), dt, description, imagej, bigtiff)
+    ny, nx = int(shape[-2]), int(shape[-1])
+    plane_bytes = ny * nx * dt.itemsize
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    arr = np.ascontiguousarray(rows, dtype=dt)
+    arr = arr.reshape((-1,) + arr.shape[-2:])
+    fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)
+    try:
+        os.ftruncate(fd, data_pos + nbytes + len(tail))
+        os.pwrite(fd, head, 0)
+        os.pwrite(fd, tail, data_pos + nbytes)
+        if arr.size:
+            for z in range(arr.shape[0]):
+                os.pwrite(fd, memoryview(arr[z].reshape(-1)).cast("B"), data_pos + z * plane_bytes + int(y0) * nx *
+                          dt.itemsize)
     finally:
         os.close(fd)
 

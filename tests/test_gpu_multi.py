@@ -62,7 +62,9 @@ def _tree(d):
 
 
 @pytest.mark.parametrize("world,parallel,shape", [(2, "frames", (9, 12, 20, 24)), (2, "zslab", (9, 12, 20, 24)),
-                                                  (3, "zslab", (7, 10, 16, 20)), (2, "auto", (7, 10, 16, 20))])
+                                                  (3, "zslab", (7, 10, 16, 20)), (2, "auto", (7, 10, 16, 20)),
+                                                  (2, "yslab", (9, 6, 40, 24)), (3, "yslab", (7, 5, 31, 20)),
+                                                  (4, "auto", (8, 4, 64, 30))])
 def test_onetif_multi_rank_equals_single(tmp_path, world, parallel, shape):
     stack = np.random.default_rng(world).integers(0, 4096, size=shape).astype(np.uint16)
     single, multi = tmp_path / "single", tmp_path / "multi"
@@ -90,6 +92,16 @@ def test_sequencet_zslab_three_ranks(tmp_path):
     for hh in range(2):
         got = [tf.imread(out / f"v_t_{n}_t{hh + 3:04d}.tiff") for n in ("vx", "vy", "vz", "rel")]
         assert_flow3d_matches_oracle(got, stack[hh:hh + 7], 1, 1, 2)
+
+
+def test_sequencet_yslab_two_ranks(tmp_path):
+    stack = np.random.default_rng(8).integers(0, 4096, size=(7, 4, 36, 18)).astype(np.uint16)
+    for t in range(7):
+        tf.imwrite(tmp_path / f"r_t{t}.tif", stack[t])
+    _run_ranks(2, (str(tmp_path), "r_t.*", "SequenceT", 3, 1, 1, 2), {"parallel": "yslab"})
+    out = tmp_path / "OpticalFlow3D" / "r_t"
+    got = [tf.imread(out / f"r_t_{n}_t0003.tiff") for n in ("vx", "vy", "vz", "rel")]
+    assert_flow3d_matches_oracle(got, stack, 1, 1, 2)
 
 
 def test_lzw_onetif_input(tmp_path):

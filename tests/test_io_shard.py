@@ -125,3 +125,30 @@ def test_exchange_frame_halo_gloo(world, nz, halo):
     for p in ps:
         p.join(timeout=60)
     assert all(res.values()) and len(res) == world
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 7])
+def test_write_rows_equals_imwrite(tmp_path, world):
+    v = np.random.default_rng(4).standard_normal((5, 19, 23))
+    tf.imwrite(tmp_path / "full.tiff", v, photometric="minisblack")
+    for r in range(world)[::-1]:
+        y0, y1 = zslab_bounds(19, r, world)
+        tf.write_rows(tmp_path / "part.tiff", v.shape, v.dtype, y0, v[:, y0:y1])
+    assert (tmp_path / "full.tiff").read_bytes() == (tmp_path / "part.tiff").read_bytes()
+
+
+def test_read_rows(tmp_path):
+    a = np.random.default_rng(5).integers(0, 60000, (4, 30, 21)).astype(np.uint16)
+    tf.imwrite(tmp_path / "u.tif", a)
+    assert np.array_equal(tf.TiffFile(tmp_path / "u.tif").read_rows(7, 19), a[:, 7:19])
+    tf.imwrite_libtiff(tmp_path / "c.tif", a, compression=5, bigtiff=False)
+    assert np.array_equal(tf.TiffFile(tmp_path / "c.tif").read_rows(0, 5), a[:, 0:5])
+
+
+def test_slab_axis_prefers_rows_for_flat_volumes():
+    from opticalflow3d_dev_amd.shard import slab_axis, slab_work
+
+    assert slab_axis(256, 1024, 4, 6, 15) == 1      # configs[3]
+    assert slab_axis(512, 2048, 8, 6, 15) == 1      # configs[4]
+    assert slab_axis(2048, 64, 4, 6, 15) == 0       # tall volume: z-slabs
+    assert slab_work(1024, 256, 4, 6, 15, 1) < 1.2  # c4 row slabs: < 20 % halo work at P = 4
