@@ -76,11 +76,11 @@ def synthetic_frames(nt, nz, ny, nx, seed):
     return out
 
 
-def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device, out=None, zchunk=32):
-    """Planes [z0, z1) of a device-generated uint16 stack of the same family as
-    synthetic_frames (for the large configs: each rank generates only its own
-    planes, and the planes do not depend on the decomposition).  Returned as
-    int16 bits (values stay below 32768); generated zchunk planes at a time so
+def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device, out=None, zchunk=32, rows=None):
+    """Planes [z0, z1) (rows [y0, y1) of them with rows=(y0, y1)) of a device-generated
+    uint16 stack of the same family as synthetic_frames (for the large configs: each rank
+    generates only its own part, and the values do not depend on the decomposition).
+    Returned as int16 bits (values stay below 32768); generated zchunk planes at a time so
     the fp64 temporaries stay small next to a c5 workspace."""
     import torch
 
@@ -89,17 +89,19 @@ def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device, out=None, zchunk=32):
     ph = rng.uniform(0, 2 * np.pi, size=(3, 3))
     vel = (0.3, -0.2, -0.1)
     f64 = dict(dtype=torch.float64, device=device)
+    ya, yb = rows if rows is not None else (0, ny)
     if out is None:
-        out = torch.empty((nt, z1 - z0, ny, nx), dtype=torch.int16, device=device)
-    y = torch.arange(ny, **f64)[None, :, None]
+        out = torch.empty((nt, z1 - z0, yb - ya, nx), dtype=torch.int16, device=device)
+    y = torch.arange(ya, yb, **f64)[None, :, None]
     x = torch.arange(nx, **f64)[None, None, :]
     for c0 in range(z0, z1, zchunk):
         c1 = min(c0 + zchunk, z1)
         z = torch.arange(c0, c1, **f64)[:, None, None]
         lin = ((torch.arange(c0, c1, device=device)[:, None, None] * ny
-                + torch.arange(ny, device=device)[None, :, None]) * nx + torch.arange(nx, device=device)[None, None, :])
+                + torch.arange(ya, yb, device=device)[None, :, None]) * nx
+               + torch.arange(nx, device=device)[None, None, :])
         for t in range(nt):
-            sv = torch.zeros((c1 - c0, ny, nx), **f64)
+            sv = torch.zeros((c1 - c0, yb - ya, nx), **f64)
             for q in range(3):
                 sv += (torch.sin(k[q, 0] * (x - vel[0] * t) + ph[q, 0])
                        * torch.sin(k[q, 1] * (y - vel[1] * t) + ph[q, 1])
@@ -320,68 +322,132 @@ def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=
     }
 
 
-def run_zslab(args, world, rank, local_rank, dev):
-    """configs[3]: ONE frame per step, z-sharded over the ranks (strong scaling).  Each rank
-    generates only its own input planes; every step fetches the rd+rw halo planes from the
-    z-neighbours (RCCL P2P over xGMI) and computes its output planes (shard.ZSlabFlow)."""
+def run_slab(args, world, rank, local_rank, dev):
+    """configs[3] / configs[4]: ONE volume per output frame, split over the ranks (strong
+    scaling), as process_flow runs a time series of it: each rank holds its own part (z-planes
+    or rows: --split, default the axis with less halo work, shard.slab_axis) of 2*rt+2
+    resident frames; a step = the newest frame's halo exchange with the neighbours (RCCL
+    P2P, on its own stream, beside the previous step's compute) + the rank's compute.
+    OF3D_BENCH_VRANK="r/P": time rank r of a P-way split on this one GPU (no exchange) —
+    the per-rank compute the scaling model in DESIGN.md uses."""
     import torch
     import torch.distributed as dist
 
-    from opticalflow3d_dev_amd import _lib, radii
-    from opticalflow3d_dev_amd.shard import ZSlabFlow
+    from opticalflow3d_dev_amd import _lib, make_taps, radii
+    from opticalflow3d_dev_amd.shard import exchange_frame_halo, halo_planes, slab_axis, zslab_bounds
 
     nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
     fp32 = args.config in FP32_CONFIGS or args.precision == "fp32"
-    zf = ZSlabFlow(nz, ny, nx, s, t, w, rank, world, device=dev.index, timing=max(args.steps, 1),
-                   mode=_lib.OF3D_FP32 if fp32 else 0)
-    own = zf.allocate(torch.int16, dev)
+    sv = 4 if fp32 else 8
+    vr = os.environ.get("OF3D_BENCH_VRANK")
+    prank, pworld = (int(v) for v in vr.split("/")) if vr else (rank, world)
+    axis = {"z": 0, "y": 1}.get(args.split, None)
+    if axis is None:
+        axis = slab_axis(nz, ny, pworld, rd, rw)
+    n_ax = nz if axis == 0 else ny
+    a0, a1 = zslab_bounds(n_ax, prank, pworld)
+    ai0, ai1 = halo_planes(n_ax, a0, a1, rd, rw) if pworld > 1 else (0, n_ax)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    taps = make_taps(s, t, w)
+    if axis == 0:
+        plan = _lib.Plan(3, nz, ny, nx, taps, device=dev.index, max_out_planes=max(a1 - a0, 1),
+                         timing=max(args.steps, 1), mode=mode)
+        blk_shape = (ai1 - ai0, ny, nx)
+    else:
+        plan = _lib.Plan(3, nz, ai1 - ai0, nx, taps, device=dev.index, timing=max(args.steps, 1), mode=mode)
+        blk_shape = (nz, ai1 - ai0, nx)
+    nblk = int(np.prod(blk_shape))
     seed = 20260206 + (5 if fp32 else 4)
-    synthetic_slab(nwin, nz, ny, nx, zf.z0, zf.z1, seed, dev, out=own)
-    n_out = max(zf.z1 - zf.z0, 0) * ny * nx
-    outs = [torch.empty(max(n_out, 1), dtype=torch.float32 if fp32 else torch.float64, device=dev) for _ in range(3)]
-    rel = torch.empty(max(n_out, 1), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # 2 rt + 2 slots: the step's exchange goes to the slot the frame before last read
+    ring = torch.empty((nwin + 1,) + blk_shape, dtype=torch.int16, device=dev)
+    for f in range(nwin + 1):
+        if axis == 0:
+            synthetic_slab(1, nz, ny, nx, ai0, ai1, seed + f, dev, out=ring[f:f + 1])
+        else:
+            synthetic_slab(1, nz, ny, nx, 0, nz, seed + f, dev, out=ring[f:f + 1], rows=(ai0, ai1))
+    n_full = nblk if axis == 1 else (a1 - a0) * ny * nx
+    vt = torch.float32 if fp32 else torch.float64
+    outs = [torch.empty(max(n_full, 1), dtype=vt, device=dev) for _ in range(3)]
+    rel = torch.empty(max(n_full, 1), dtype=torch.float32, device=dev)
+    comp = torch.cuda.current_stream(dev)
+    xs = torch.cuda.Stream(device=dev)
+    done = {}  # slot -> event of the last compute that read it
+    order = list(range(nwin))
+    state = {"k": 0}
+
+    def xchg_view(slot):
+        v = ring[slot]
+        return v if axis == 0 else v.transpose(0, 1)
 
     def step():
-        zf.run(_lib.OF3D_U16, *outs, rel, stream)
+        k = state["k"]
+        state["k"] += 1
+        new = (order[-1] + 1) % (nwin + 1)  # the free slot takes the newest frame
+        if world > 1 and not vr:
+            with torch.cuda.stream(xs):
+                if new in done:
+                    xs.wait_event(done[new])
+                exchange_frame_halo(xchg_view(new), ai0, a0, a1, n_ax, rd + rw, rank, world)
+                ev = torch.cuda.Event()
+                ev.record(xs)
+            comp.wait_event(ev)
+        order.pop(0)
+        order.append(new)
+        ptrs = [ring[sl].data_ptr() for sl in order]
+        if axis == 0:
+            plan.execute(ptrs, _lib.OF3D_U16, ai0, a0, a1, outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
+                         rel.data_ptr(), comp.cuda_stream)
+        else:
+            plan.execute(ptrs, _lib.OF3D_U16, 0, 0, nz, outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
+                         rel.data_ptr(), comp.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(comp)
+        for sl in order:
+            done[sl] = ev
+        del k
 
-    elapsed, profile, dom, dom_ms = timed_region(step, zf.runner.plan if zf.runner is not None else None, args,
-                                                 world, dev)
-    finite = bool(torch.isfinite(outs[0][:n_out]).all().item()) if n_out else True
+    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
+    finite = bool(torch.isfinite(outs[0][:n_full]).all().item()) if n_full else True
     if world > 1:
         elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
         finite = bad == 0.0
     if rank == 0:
         vox = nz * ny * nx
-        nb, no = zf.zi1 - zf.zi0, zf.z1 - zf.z0
-        ng = min(zf.z1 + rw, nz) - max(zf.z0 - rw, 0)
-        sv = 4 if fp32 else 8
-        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, ny * nx, sv),
-                        args.config, (nwin * 2 + 3 * sv + 4) * no * ny * nx,
-                        frame_ops_per_voxel(rd, rs, rt, rw) * no * ny * nx, nwin, sv)
-        roof["frame"]["note"] = "rank 0's slab (output planes %d..%d, input planes %d..%d)" % (
-            zf.z0, zf.z1, zf.zi0, zf.zi1)
+        own = (a1 - a0) * (ny * nx if axis == 0 else nz * nx)
+        if axis == 0:
+            nb, no, ng = ai1 - ai0, a1 - a0, min(a1 + rw, nz) - max(a0 - rw, 0)
+            plane = ny * nx
+        else:
+            nb = no = ng = nz
+            plane = (ai1 - ai0) * nx
+        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, plane, sv), args.config,
+                        (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv)
+        roof["frame"]["note"] = "this rank's share: %s %d..%d (with halo %d..%d) of %d" % (
+            "planes" if axis == 0 else "rows", a0, a1, ai0, ai1, n_ax)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not vr and not args.no_cpu_baseline:
             sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
             host = synthetic_slab(nwin, nz, ny, nx, 0, sub, seed, dev).cpu().numpy().view(np.uint16)
             cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
+        split = ("z-slabs" if axis == 0 else "row slabs")
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
-            "value": round(vox * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32" if fp32 else "f64",
-            "data": "synthetic",
+            "value": round((own if vr else vox) * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32" if fp32 else "f64", "data": "synthetic",
             "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
-                       "wSig": w, "parallelism": f"z-slabs x{world}, halo {rd + rw} planes" if world > 1
-                       else "single GPU (whole frame)", "inputs": "own z-planes of 2*rt+1 uint16 frames "
-                       "resident in HBM; halo exchange inside the timed step", "outputs_finite": finite},
+                       "wSig": w,
+                       "parallelism": (f"virtual rank {prank} of {pworld} ({split}, compute only)" if vr else
+                                       f"{split} x{world}, halo {rd + rw}" if world > 1 else "single GPU (whole frame)"),
+                       "inputs": "own part of 2*rt+2 uint16 frames resident in HBM; per step the newest frame's "
+                                 "halo exchange (RCCL P2P, own stream) + compute", "outputs_finite": finite},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    zf.close()
+    plan.close()
 
 
 def main():
@@ -395,6 +461,8 @@ def main():
     ap.add_argument("--overlap", type=int, default=int(os.environ.get("OF3D_BENCH_OVERLAP", "-1")),
                     help="z chunk (output planes) of the plan's overlap mode; 0 = serial; -1 = the plan's default")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
+    ap.add_argument("--split", default="auto", choices=("auto", "z", "y"),
+                    help="c4/c5: split axis of the volume over the ranks (auto: less halo work)")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
                     help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
     args = ap.parse_args()
@@ -422,7 +490,7 @@ def main():
         else:
             dist.init_process_group(backend)
     if args.config in ZSLAB_CONFIGS:
-        run_zslab(args, world, rank, local_rank, dev)
+        run_slab(args, world, rank, local_rank, dev)
         if world > 1:
             dist.destroy_process_group()
         return
