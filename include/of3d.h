@@ -90,6 +90,11 @@ const char* of3d_last_error(void);
 /* Number of visible HIP devices (0 when no GPU / no driver). */
 int of3d_device_count(void);
 
+/* Free the plans the host entry points cache (of3d_flow3d / of3d_flow2d keep the device
+ * workspace of their last two shapes resident; tens of GB at configs[3]).  No reference
+ * counterpart (calc_flow3D allocates per call). */
+int of3d_cache_clear(void);
+
 /* ---- host entry points (replace calc_flow3D / calc_flow2D) -------------- */
 
 /* calc_flow3D (calc_flow.py:175-360).  images: (nt, nz, ny, nx) of `dtype`;

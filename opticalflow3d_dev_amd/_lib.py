@@ -37,7 +37,7 @@ EXPORTED = (
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
-    "of3d_plan_set_overlap",
+    "of3d_plan_set_overlap", "of3d_cache_clear",
 )
 
 
@@ -89,6 +89,7 @@ def load():
         lib.of3d_version.restype = ctypes.c_int
         lib.of3d_last_error.restype = ctypes.c_char_p
         lib.of3d_device_count.restype = ctypes.c_int
+        lib.of3d_cache_clear.restype = ctypes.c_int
         lib.of3d_flow3d.argtypes = [P, ctypes.c_int, i64, i64, i64, i64, ctypes.POINTER(Taps), ctypes.c_int,
                                     ctypes.c_int, D, D, D, P, ctypes.POINTER(Perf)]
         lib.of3d_flow3d.restype = ctypes.c_int
@@ -126,6 +127,11 @@ def load():
         lib.of3d_dma_copy.restype = ctypes.c_int
         _lib = lib
         return lib
+
+
+def cache_clear():
+    """of3d_cache_clear: release the device workspaces cached by calc_flow3D / calc_flow2D."""
+    check(load().of3d_cache_clear())
 
 
 def last_error() -> str:

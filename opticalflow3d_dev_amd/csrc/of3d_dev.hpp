@@ -1704,6 +1704,71 @@ constexpr int k5c_groups(int rw, int r) {
     return (k5c_zc(r) + 2 * rw + rpwi - 1) / rpwi;
 }
 
+// ---------------------------------------------------------------------------
+// General-radius path (any xyzSig / wSig the reference accepts, calc_flow.py:230-267,
+// beyond the tiled kernels' LDS limits): every 1-D pass as its own streaming kernel
+// straight from global memory (L2), one output per thread, the same scipy order and
+// global-edge clamping; products and solves pointwise.  Not tuned: it exists so that no
+// parameter the reference takes is refused.
+// ---------------------------------------------------------------------------
+template <typename T, typename F>
+__global__ __launch_bounds__(256) void k_cast_gen(const T* __restrict__ in, F* __restrict__ out, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) out[i] = (F)in[i];
+}
+
+// out[q] (planes [q0, q1), origin out_z0) = pass along `axis` (0 x, 1 y, 2 z) of in (origin
+// in_z0); z indices clamp to [0, zhi); half taps h[0..r] (h[k] = w[r - k]); anti: lo - hi
+template <typename F>
+__global__ __launch_bounds__(256) void k_corr_gen(const F* __restrict__ in, int in_z0, F* __restrict__ out, int out_z0,
+                                                  int q0, int q1, int ny, int nx, int axis, const F* __restrict__ h,
+                                                  int r, int anti, int zhi) {
+    const size_t plane = (size_t)ny * nx, n = (size_t)(q1 - q0) * plane;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int q = q0 + (int)(i / plane);
+        const size_t rem = i % plane;
+        const int y = (int)(rem / nx), x = (int)(rem % nx);
+        auto at = [&](int d) -> F {
+            int zz = q, yy = y, xx = x;
+            if (axis == 0)
+                xx = clampi(x + d, 0, nx - 1);
+            else if (axis == 1)
+                yy = clampi(y + d, 0, ny - 1);
+            else
+                zz = clampi(q + d, 0, zhi - 1);
+            return in[(size_t)(zz - in_z0) * plane + (size_t)yy * nx + xx];
+        };
+        F o = at(0) * h[0];
+        for (int k = r; k >= 1; --k) o = o + (anti ? (at(-k) - at(k)) : (at(-k) + at(k))) * h[k];
+        out[(size_t)(q - out_z0) * plane + rem] = o;
+    }
+}
+
+// the structure-tensor products (tables as k_prod_wyx): P[p] = G[a(p)] * G[b(p)], n points
+template <typename F>
+__global__ __launch_bounds__(256) void k_prod_gen(const F* __restrict__ G, F* __restrict__ P, size_t fs, size_t n,
+                                                  int np) {
+    const unsigned long long pa = np == 9 ? 0x311222312ull : 0x12212ull, pb = np == 9 ? 0x313231000ull : 0x12100ull;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        for (int p = 0; p < np; ++p)
+            P[p * fs + i] = G[((pa >> (4 * p)) & 15u) * fs + i] * G[((pb >> (4 * p)) & 15u) * fs + i];
+}
+
+// 3D solve + reliability from the nine windowed fields (order tx ty tz xy xz x2 yz y2 z2)
+template <typename F, typename RelT>
+__global__ __launch_bounds__(256) void k_solve3_gen(const F* __restrict__ W, size_t fs, size_t n, F* __restrict__ vx,
+                                                    F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const double tx = W[i], ty = W[fs + i], tz = W[2 * fs + i], xy = W[3 * fs + i], xz = W[4 * fs + i],
+                     x2 = W[5 * fs + i], yz = W[6 * fs + i], y2 = W[7 * fs + i], z2 = W[8 * fs + i];
+        double ox, oy, oz;
+        solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
+        vx[i] = (F)ox;
+        vy[i] = (F)oy;
+        vz[i] = (F)oz;
+        rel[i] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
+    }
+}
+
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
 template <typename F>
 __global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t fs, int n, F* __restrict__ vx,

@@ -61,6 +61,7 @@ struct of3d_plan {
     bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
     bool k2c = true;  // z-march K2 where instantiated (OF3D_K2C=0: k_grad_z)
     bool k12 = true;  // fused gradient kernel where instantiated (OF3D_K12=0: K1c + K2c)
+    bool general = false;  // radii beyond the tiled kernels' limits: the general-radius path
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
@@ -99,7 +100,7 @@ namespace {
 int build_taps(const of3d_taps* t, of3d_plan* p) {
     if (!t || !t->gauss || !t->deriv || !t->smooth || !t->tderiv || !t->window) return fail("of3d: null taps");
     if (t->rd < 0 || t->rs < 0 || t->rt < 0 || t->rw < 0) return fail("of3d: negative tap radius");
-    if (t->rd > kMaxR || t->rs > kMaxR || t->rw > kMaxR) return fail("of3d: spatial tap radius exceeds 48");
+    if (t->rd > 4096 || t->rs > 4096 || t->rw > 4096) return fail("of3d: spatial tap radius exceeds 4096");
     if (2 * t->rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
     struct {
         const double* w;
@@ -330,9 +331,16 @@ int k34_tune(of3d_plan* p) {
     F* G = (F*)(p->ndim == 3 ? p->Y : p->X);
     F* P = (F*)(p->ndim == 3 ? p->X : p->Y);
     const F* hw = dev_taps<F>(p).w;
-    hipEvent_t e0, e1;
-    OF3D_HIP(hipEventCreate(&e0));
-    OF3D_HIP(hipEventCreate(&e1));
+    struct Events {  // destroyed on every path out
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        ~Events() {
+            if (e0) (void)hipEventDestroy(e0);
+            if (e1) (void)hipEventDestroy(e1);
+        }
+    } ev;
+    OF3D_HIP(hipEventCreate(&ev.e0));
+    OF3D_HIP(hipEventCreate(&ev.e1));
+    hipEvent_t e0 = ev.e0, e1 = ev.e1;
     // the heuristic pick (k34_setup) stays unless another shape is >= 3 % faster: stable
     // choices from run to run (candidates within noise of each other otherwise flip)
     size_t h0 = 0;
@@ -356,8 +364,6 @@ int k34_tune(of3d_plan* p) {
         }
         if (i == 0 ? true : ms < 0.97f * best) best = ms, bi = i;
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     p->k34 = p->k34_cand[bi];
     if (getenv("OF3D_VERBOSE"))
         fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d (%.3f ms)\n", p->k34_cand.size(),
@@ -406,8 +412,23 @@ int set_attrs_t(of3d_plan* p) {
     return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
 }
 
+// Radii the tiled kernels cannot stage (the legacy K1's 64-wide strips need rd <= 24, every
+// tile at most 160 KiB of LDS, kMaxR for the tap padding) run the general-radius path
+// (k_corr_gen passes: the same arithmetic, any radius).  OF3D_GENERAL=1 forces it (tests).
+bool needs_general(const of3d_plan* p) {
+    if (const char* e = getenv("OF3D_GENERAL"); e && e[0] == '1') return true;
+    if (p->rd > 24 || p->rs > kMaxR || p->rw > kMaxR) return true;
+    const size_t e = p->fp32 ? 4 : 8, lim = 160 * 1024;
+    const size_t k3 = (size_t)(K3_STEP + 2 * p->rw) * 64 * e;
+    const size_t k4 = (size_t)K4_ROWS * (((K4_TX + 2 * k4_halo(p->rw)) | 1) + (K4_TX + 1)) * e;
+    const size_t k5 = (size_t)2 * (k5_geom(p->rw).g * k5_geom(p->rw).r + 2 * p->rw) * 64 * e;
+    const size_t k2 = (size_t)(K2_ZC + 2 * std::max(p->rd, p->rs)) * 64 * e;
+    return k3 > lim || k4 > lim || k5 > lim || k2 > lim;
+}
+
 int set_attrs(of3d_plan* p) {
-    if (p->rd > 24) return fail("of3d: xyzSig too large (derivative radius > 24)");
+    p->general = needs_general(p);
+    if (p->general) return 0;
     return p->fp32 ? set_attrs_t<float>(p) : set_attrs_t<double>(p);
 }
 
@@ -429,6 +450,119 @@ Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
     r.zb0 = std::max<int64_t>(r.zg0 - p->rd, 0);
     r.zb1 = std::min<int64_t>(r.zg1 + p->rd, p->nz);
     return r;
+}
+
+// General-radius pipeline (any radius; see needs_general).  3D workspace use: Y0 dt0, Y1 the
+// centre frame in F, X0..2 the y passes, Y2..5 the x passes (pre-z), X0..3 the gradients,
+// Y0..8 the products, X0..8 W-y, Y0..8 W-x, X0..8 W-z; 2D the same without z.  Plane ranges
+// and clamping as the tiled pipeline: inputs [zb0, zb1), gradients / products [zg0, zg1)
+// (z pass clamped at zb1), outputs [zo0, zo1) (W z clamped at zg1).  Stage events: grad_xy
+// = dt0 + y / x passes, grad_z = gradient z pass, prod_wy = products + W y + W x, wz_solve.
+template <typename F, typename Mark>
+int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, const Ranges& R, F* vx, F* vy, F* vz,
+                void* rel, hipStream_t st, Mark& mark) {
+    const bool d3 = p->ndim == 3;
+    const int ny = (int)p->ny, nx = (int)p->nx;
+    const size_t plane = (size_t)ny * nx, fs = p->fs, es = dtype_size(dtype);
+    F* X = (F*)p->X;
+    F* Y = (F*)p->Y;
+    const DevTaps<F> tp = dev_taps<F>(p);
+    auto grid = [&](size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 256 * 64)); };
+    const int zb0 = (int)R.zb0, zb1 = (int)R.zb1, zg0 = (int)R.zg0, zg1 = (int)R.zg1, zo0 = (int)R.zo0,
+              zo1 = (int)R.zo1;
+    auto pass = [&](const F* in, int in_z0, F* out, int out_z0, int q0, int q1, int axis, const F* h, int r, int anti,
+                    int zhi) -> int {
+        if (q1 <= q0) return 0;
+        hipLaunchKernelGGL(k_corr_gen<F>, grid((size_t)(q1 - q0) * plane), dim3(256), 0, st, in, in_z0, out, out_z0, q0,
+                           q1, ny, nx, axis, h, r, anti, zhi);
+        OF3D_HIP(hipGetLastError());
+        return 0;
+    };
+    if (mark(0)) return -1;
+    // dt0 (the streaming K0 for any rt) and the centre frame as F, planes [zb0, zb1)
+    {
+        size_t off0 = (size_t)(zb0 - frame_z0) * plane, n = (size_t)(zb1 - zb0) * plane;
+        long long fstride = 0;
+        int rt_arg = p->rt;
+        F* D0 = Y;
+        const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
+        void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
+        OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
+        const void* Ic = (const char*)fr.p[p->rt] + off0 * es;
+        F* If = Y + fs;
+        switch (dtype) {
+#define OF3D_CAST(C, T)                                                                                         \
+    case C:                                                                                                     \
+        hipLaunchKernelGGL((k_cast_gen<T, F>), grid(n), dim3(256), 0, st, (const T*)Ic, If, n);                   \
+        break;
+            OF3D_CAST(OF3D_U8, uint8_t)
+            OF3D_CAST(OF3D_U16, uint16_t)
+            OF3D_CAST(OF3D_I16, int16_t)
+            OF3D_CAST(OF3D_U32, uint32_t)
+            OF3D_CAST(OF3D_I32, int32_t)
+            OF3D_CAST(OF3D_F32, float)
+            OF3D_CAST(OF3D_F64, double)
+#undef OF3D_CAST
+            default: return fail("of3d: unsupported dtype");
+        }
+        OF3D_HIP(hipGetLastError());
+    }
+    const int pz0 = zb0, pz1 = zb1;  // planes of the y / x passes (3D: the input range; 2D: plane 0)
+    // y passes: A1 = y(G)[dt0], A2 = y(D)[I], A3 = y(S)[I]
+    if (pass(Y, pz0, X, pz0, pz0, pz1, 1, tp.g, p->rd, 0, 1) || pass(Y + fs, pz0, X + fs, pz0, pz0, pz1, 1, tp.d, p->rd, 1, 1) ||
+        pass(Y + fs, pz0, X + 2 * fs, pz0, pz0, pz1, 1, tp.s, p->rs, 0, 1))
+        return -1;
+    // x passes: B1 = x(G)[A1] (dt), B2 = x(S)[A2] (dy), B3 = x(D)[A3] (dx), B4 = x(S)[A3] (pre-z dz)
+    if (pass(X, pz0, Y + 2 * fs, pz0, pz0, pz1, 0, tp.g, p->rd, 0, 1) ||
+        pass(X + fs, pz0, Y + 3 * fs, pz0, pz0, pz1, 0, tp.s, p->rs, 0, 1) ||
+        pass(X + 2 * fs, pz0, Y + 4 * fs, pz0, pz0, pz1, 0, tp.d, p->rd, 1, 1) ||
+        (d3 && pass(X + 2 * fs, pz0, Y + 5 * fs, pz0, pz0, pz1, 0, tp.s, p->rs, 0, 1)))
+        return -1;
+    if (mark(1)) return -1;
+    const F* Gr;
+    int gz0, gz1;
+    if (d3) {  // z passes into X0..3 over [zg0, zg1): dt G, dy S, dx S, dz D
+        if (pass(Y + 2 * fs, zb0, X, zg0, zg0, zg1, 2, tp.g, p->rd, 0, zb1) ||
+            pass(Y + 3 * fs, zb0, X + fs, zg0, zg0, zg1, 2, tp.s, p->rs, 0, zb1) ||
+            pass(Y + 4 * fs, zb0, X + 2 * fs, zg0, zg0, zg1, 2, tp.s, p->rs, 0, zb1) ||
+            pass(Y + 5 * fs, zb0, X + 3 * fs, zg0, zg0, zg1, 2, tp.d, p->rd, 1, zb1))
+            return -1;
+        Gr = X;
+        gz0 = zg0, gz1 = zg1;
+    } else {
+        Gr = Y + 2 * fs;  // dt, dy, dx
+        gz0 = 0, gz1 = 1;
+    }
+    if (mark(2)) return -1;
+    const int np = d3 ? 9 : 5;
+    F* Pp = d3 ? Y : X;  // products
+    F* Wy = d3 ? X : Y;
+    {
+        const size_t n = (size_t)(gz1 - gz0) * plane;
+        hipLaunchKernelGGL(k_prod_gen<F>, grid(n), dim3(256), 0, st, Gr, Pp, fs, n, np);
+        OF3D_HIP(hipGetLastError());
+    }
+    for (int f = 0; f < np; ++f)
+        if (pass(Pp + f * fs, gz0, Wy + f * fs, gz0, gz0, gz1, 1, tp.w, p->rw, 0, 1) ||
+            pass(Wy + f * fs, gz0, Pp + f * fs, gz0, gz0, gz1, 0, tp.w, p->rw, 0, 1))
+            return -1;
+    if (mark(3) || mark(4)) return -1;  // W-xy in Pp ("wx" stays folded into "prod_wy")
+    if (d3) {
+        for (int f = 0; f < 9; ++f)
+            if (pass(Pp + f * fs, zg0, X + f * fs, zo0, zo0, zo1, 2, tp.w, p->rw, 0, zg1)) return -1;
+        const size_t n = (size_t)(zo1 - zo0) * plane;
+        if (p->rel64)
+            hipLaunchKernelGGL((k_solve3_gen<F, double>), grid(n), dim3(256), 0, st, (const F*)X, fs, n, vx, vy, vz,
+                               (double*)rel);
+        else
+            hipLaunchKernelGGL((k_solve3_gen<F, float>), grid(n), dim3(256), 0, st, (const F*)X, fs, n, vx, vy, vz,
+                               (float*)rel);
+    } else {
+        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv((int64_t)plane, 256)), dim3(256), 0, st, (const F*)Pp, fs,
+                           (int)plane, vx, vy, (F*)rel);
+    }
+    OF3D_HIP(hipGetLastError());
+    return mark(5);
 }
 
 // The stage pipeline over output planes [zo0, zo1).  Stage launches take plane sub-ranges:
@@ -686,6 +820,20 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const int slot = p->timing_slots ? (int)(p->tcount % p->timing_slots) : 0;
     hipEvent_t* evs = p->host_ev ? p->ev : (p->timing_slots ? &p->tev[(size_t)slot * p->tev_per_slot] : nullptr);
     const unsigned tmask = p->host_ev ? (1u << kStages) - 1 : p->timing_mask;
+    if (p->general) {
+        const unsigned bmask = tmask | (tmask << 1);
+        auto mark = [&](int i) -> int {
+            if (evs && ((bmask >> i) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s));
+            return 0;
+        };
+        if (run_general<F>(p, fr, dtype, frame_z0, R, vx, vy, vz, rel, s, mark)) return -1;
+        if (!p->host_ev && p->timing_slots) {
+            p->tchunks[slot] = 0;
+            ++p->tcount;
+        }
+        p->stages_run = kStages;
+        return 0;
+    }
     const bool one_stage = evs && !p->host_ev && (tmask & (tmask - 1)) == 0;
     // overlap only with the fused K34, and with no per-stage profile requested
     const int64_t nout = R.zo1 - R.zo0;
@@ -757,6 +905,8 @@ int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, 
                    : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
 }
 
+void plan_free(of3d_plan* p);
+
 int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
                 int device, int64_t max_out_planes) {
     if (!out) return fail("of3d: null plan pointer");
@@ -766,7 +916,14 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     if (ndim == 2 && nz != 1) return fail("of3d: 2D plans need nz == 1");
     if (nz < 1 || ny < 1 || nx < 1) return fail("of3d: empty volume");
     if (ny * nx > (int64_t)INT32_MAX || nz > 65535) return fail("of3d: volume too large for one plan");
-    std::unique_ptr<of3d_plan> p(new of3d_plan);
+    // every error path below frees whatever the plan holds so far (plan_free takes partial plans)
+    struct Owner {
+        of3d_plan* p = new of3d_plan;
+        ~Owner() { plan_free(p); }
+        of3d_plan* get() const { return p; }
+        of3d_plan* operator->() const { return p; }
+        of3d_plan* release() { of3d_plan* q = p; p = nullptr; return q; }
+    } p;
     p->ndim = ndim;
     p->rel64 = (mode & OF3D_REL_F64) != 0;
     p->fp32 = (mode & OF3D_FP32) != 0;
@@ -990,6 +1147,13 @@ __global__ __launch_bounds__(256) void k_copy_bytes(const unsigned char* __restr
 extern "C" {
 
 int of3d_version(void) { return OF3D_VERSION; }
+
+int of3d_cache_clear(void) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (auto& e : g_cache) plan_free(e.plan);
+    g_cache.clear();
+    return 0;
+}
 
 const char* of3d_last_error(void) { return g_err.c_str(); }
 

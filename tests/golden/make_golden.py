@@ -10,6 +10,7 @@ reference's vx/vy/[vz]/rel, plus the fp64 eigenvalue range of the restated
 tensor (for the tighter 3D rel check).  No reference source is copied.
 
 Usage:  python tests/golden/make_golden.py      (writes tests/golden/*.npz)
+        python tests/golden/make_golden.py --only c3d_big_xyzsig9,c2d_big_sigmas   (just those)
 """
 
 import json
@@ -59,6 +60,12 @@ CASES_3D = [
     ("c3d_frac_sigmas", lambda: rand_u16((7, 6, 16, 18), 9), (1.5, 1, 2.5)),
     ("c3d_nonsquare_odd", lambda: rand_u16((7, 5, 9, 33), 10), (1, 1, 3)),
     ("c3d_default_params", lambda: rand_u16((7, 8, 14, 18), 12), (3, 1, 4)),
+    # round 2: the reference accepts any sigma (calc_flow.py:230-267): radii past the
+    # tiled kernels' limits (rd 27 > 24, rw 51 > 48) run the general-radius path
+    ("c3d_big_xyzsig9", lambda: rand_u16((7, 6, 30, 34), 13), (9, 1, 2)),
+    ("c3d_big_wsig17", lambda: rand_u16((7, 5, 24, 26), 14), (1, 1, 17)),
+    # the published benchmark's parameters (PFS/plot_figureS4_computation.ipynb) at Nz = 4
+    ("c3d_pub_s3t1w4_nz4", lambda: rand_u16((7, 4, 40, 48), 15), (3, 1, 4)),
 ]
 
 CASES_2D = [
@@ -69,6 +76,7 @@ CASES_2D = [
     ("c2d_c2params", lambda: rand_u16((13, 30, 40), 24), (2, 2, 5)),
     ("c2d_smooth_translate", lambda: cpu_ref.synthetic_stack_np((7, 40, 36), seed=25), (1, 1, 3)),
     ("c2d_nonsquare", lambda: rand_u16((7, 3, 50), 26), (1, 1, 2)),
+    ("c2d_big_sigmas", lambda: rand_u16((7, 40, 44), 27), (9, 1, 17)),
 ]
 
 ERROR_CASES = [
@@ -83,9 +91,18 @@ ERROR_CASES = [
 
 
 def main():
+    only = None
+    if "--only" in sys.argv:  # regenerate just these cases (the others' files stay as they are)
+        only = set(sys.argv[sys.argv.index("--only") + 1].split(","))
     ref = load_reference()
     manifest = {}
+    mpath = os.path.join(HERE, "manifest.json")
+    if only and os.path.exists(mpath):
+        with open(mpath) as f:
+            manifest = json.load(f)
     for name, build, (s, t, w) in CASES_3D:
+        if only and name not in only:
+            continue
         img = build()
         vx, vy, vz, rel = ref.calc_flow3D(img, s, t, w)
         st = cpu_ref.structure_tensor3d(img, s, t, w, backend="restated")
@@ -100,6 +117,8 @@ def main():
                           "rel_dtype": str(rel.dtype)}
         print(name, img.shape, rel.dtype)
     for name, build, (s, t, w) in CASES_2D:
+        if only and name not in only:
+            continue
         img = build()
         with np.errstate(invalid="ignore"):
             vx, vy, rel = ref.calc_flow2D(img, s, t, w)
@@ -109,6 +128,10 @@ def main():
         manifest[name] = {"dims": 2, "shape": list(img.shape), "dtype": str(img.dtype), "params": [s, t, w],
                           "rel_dtype": str(rel.dtype)}
         print(name, img.shape, rel.dtype)
+    if only:
+        with open(mpath, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return
     errors = {}
     for name, dims, shape, tsig in ERROR_CASES:
         fn = ref.calc_flow3D if dims == 3 else ref.calc_flow2D

@@ -22,7 +22,8 @@ from oracle import cpu_ref
 pytestmark = pytest.mark.gpu
 
 ZSLAB_GOLDEN = ["c3d_rand_c2params", "c3d_rand_c3params", "c3d_nz1", "c3d_nz2", "c3d_nz3", "c3d_nz4",
-                "c3d_default_params", "c3d_smooth_translate", "c3d_frac_sigmas"]
+                "c3d_default_params", "c3d_smooth_translate", "c3d_frac_sigmas", "c3d_big_wsig17",
+                "c3d_pub_s3t1w4_nz4"]
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -120,14 +121,16 @@ def _smooth(shape, seed):
 
 
 @pytest.mark.parametrize("name", ["c3d_smooth_translate", "c3d_float32_nt11", "c3d_rand_c2params",
-                                  "c3d_rand_c3params", "c3d_default_params", "c3d_flat"])
+                                  "c3d_rand_c3params", "c3d_default_params", "c3d_flat", "c3d_big_xyzsig9",
+                                  "c3d_big_wsig17", "c3d_pub_s3t1w4_nz4"])
 def test_fp32_3d_vs_golden(name):
     g = load_golden(name)
     got = calc_flow3D_fp32(g["images"], g["sig"], g["tsig"], g["wsig"])
     _assert_fp32_close(got, (g["vx"], g["vy"], g["vz"]), g["rel"])
 
 
-@pytest.mark.parametrize("name", ["c2d_smooth_translate", "c2d_c1params", "c2d_c2params", "c2d_float32"])
+@pytest.mark.parametrize("name", ["c2d_smooth_translate", "c2d_c1params", "c2d_c2params", "c2d_float32",
+                                  "c2d_big_sigmas"])
 def test_fp32_2d_vs_golden(name):
     g = load_golden(name)
     got = calc_flow2D_fp32(g["images"], g["sig"], g["tsig"], g["wsig"])

@@ -156,3 +156,47 @@ def test_golden_3d_fused_gradients(name, monkeypatch):
 def test_seeded_3d_fused_gradients(case, monkeypatch):
     monkeypatch.setenv("OF3D_K12", "1")
     test_seeded_3d_vs_oracle(case)
+
+
+@pytest.fixture
+def general_path(monkeypatch):
+    """OF3D_GENERAL=1: every plan runs the general-radius kernels (k_corr_gen passes); the
+    host entry's cached plans are dropped before and after."""
+    from opticalflow3d_dev_amd import _lib
+
+    _lib.cache_clear()
+    monkeypatch.setenv("OF3D_GENERAL", "1")
+    yield
+    monkeypatch.delenv("OF3D_GENERAL")
+    _lib.cache_clear()
+
+
+@pytest.mark.parametrize("name", golden_cases("c3d"))
+def test_golden_3d_general_path(name, general_path):
+    g = load_golden(name)
+    vx, vy, vz, rel = calc_flow3D(g["images"], g["sig"], g["tsig"], g["wsig"])
+    assert bits_equal(vx, g["vx"]) and bits_equal(vy, g["vy"]) and bits_equal(vz, g["vz"])
+    assert_rel_close(rel, g["rel"], g["lmax64"], REL_TOL_REF)
+
+
+@pytest.mark.parametrize("name", golden_cases("c2d"))
+def test_golden_2d_general_path(name, general_path):
+    g = load_golden(name)
+    vx, vy, rel = calc_flow2D(g["images"], g["sig"], g["tsig"], g["wsig"])
+    for a, k in ((vx, "vx"), (vy, "vy"), (rel, "rel")):
+        assert bits_equal(a, g[k]), k
+
+
+@pytest.mark.parametrize("case", [0, 1, 3, 8, 10])
+def test_seeded_3d_general_path(case, general_path):
+    test_seeded_3d_vs_oracle(case)
+
+
+def test_zslabs_general_path(general_path):
+    """z-slab plans on the general path: plane ranges and clamping as the tiled pipeline."""
+    from opticalflow3d_dev_amd.shard import flow3d_zslabs_host
+
+    g = load_golden("c3d_big_xyzsig9")
+    for world in (2, 3):
+        vx, vy, vz, rel = flow3d_zslabs_host(g["images"], g["sig"], g["tsig"], g["wsig"], world)
+        assert bits_equal(vx, g["vx"]) and bits_equal(vy, g["vy"]) and bits_equal(vz, g["vz"])
