@@ -1697,6 +1697,88 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c(const F* __r
     if (x >= nx) return;
     k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
+// K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
+// float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each
+// rounded as the scalar op — bit-identical to k_wz_solve_c<float>), so a block covers 64
+// columns and the window layout in bytes is exactly the fp64 kernel's (rows of 32 8-byte
+// elements).  The solve and the eigenvalue stay per column in fp64.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <typename RelT, int RW, int NB, int R>
+__global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float* __restrict__ Q, int zq0, int nz, int ny,
+                                                                   int nx, size_t fs, const float* __restrict__ hw,
+                                                                   int zo0, int nzo, float* __restrict__ vx,
+                                                                   float* __restrict__ vy, float* __restrict__ vz,
+                                                                   RelT* __restrict__ rel) {
+    using V = f32x2;
+    constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // lane-columns (2 columns each), waves, z-groups per wave
+    constexpr int ZC = NW * LPC * R;
+    constexpr int H = ZC + 2 * RW;
+    constexpr int LPR = 16;                    // lanes per window row (256 B = 64 floats)
+    constexpr int RPWI = 64 / LPR;             // window rows per wave-instruction (1 KiB)
+    constexpr int HG = (H + RPWI - 1) / RPWI;  // row groups per window
+    constexpr int NJ2 = (HG + NW - 1) / NW;    // row groups per wave
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    V* sm = reinterpret_cast<V*>(smem_raw);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = lane % CB, gz = w * LPC + lane / CB;
+    const int x = blockIdx.x * 2 * CB + 2 * col;  // the lane's first column
+    const int y = blockIdx.y;
+    const int zc0 = zo0 + blockIdx.z * ZC;
+    const size_t ps = (size_t)ny * nx;
+    const int xc = min((int)blockIdx.x * 2 * CB + 4 * (lane % LPR), nx - 4);  // this lane's DMA floats
+    const float* qrow = Q + (size_t)y * nx + xc;
+    const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
+    V h[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k) h[k] = (V)(hw[k]);
+    auto issue = [&](int f, int b) {
+        const float* q = qrow + f * fs;
+        const unsigned lb = lds0 + (unsigned)(b * HG * 1024);
+#pragma unroll
+        for (int j = 0; j < NJ2; ++j) {
+            const int pg = min(w + NW * j, HG - 1);
+            const int row = min(RPWI * pg + lane / LPR, H - 1);
+            const float* src = q + (size_t)(clampi(zc0 - RW + row, 0, nz - 1) - zq0) * ps;
+            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(pg * 1024)));
+        }
+    };
+    V acc[9][R];
+#pragma unroll
+    for (int f = 0; f < NB - 1; ++f) issue(f, f);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+        const int ahead = min(NB - 2, 8 - f);
+        if (ahead >= 2)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * NJ2) : "memory");
+        else if (ahead == 1)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NJ2) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
+        lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
+#pragma unroll
+        for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
+    }
+    if (x >= nx) return;
+    const int z0l = zc0 + gz * R - zo0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        if (z0l + i >= nzo) break;
+        const size_t o = (size_t)(z0l + i) * ps + (size_t)y * nx + x;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            if (x + e >= nx) break;
+            const double tx = acc[0][i][e], ty = acc[1][i][e], tz = acc[2][i][e], xy = acc[3][i][e],
+                         xz = acc[4][i][e], x2 = acc[5][i][e], yz = acc[6][i][e], y2 = acc[7][i][e], z2 = acc[8][i][e];
+            double ox, oy, oz;
+            solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
+            vx[o + e] = (float)ox;
+            vy[o + e] = (float)oy;
+            vz[o + e] = (float)oz;
+            rel[o + e] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
+        }
+    }
+}
 constexpr int k5c_zc(int r) { return 8 * r; }  // output planes per K5c block (R planes per z-group)
 template <typename F>
 constexpr int k5c_groups(int rw, int r) {

@@ -66,6 +66,7 @@ struct of3d_plan {
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
+    bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -282,10 +283,26 @@ int k34_setup(of3d_plan* p, int np) {
 template <typename F>
 int k5c_setup(of3d_plan* p) {
     p->k5c = nullptr;
+    p->k5c_pk = false;
     if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
     if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
     const char* er = getenv("OF3D_K5C_R");
     const int r = er ? atoi(er) : 8;
+    // fp32: the packed kernel (two columns per lane as float2; window bytes as the fp64 kernel's)
+    const void* pk = nullptr;
+    if constexpr (sizeof(F) == 4) {
+        const size_t buf2 = (size_t)k5c_groups<double>(p->rw, r) * 1024;
+        const int nb2 = 2 * 3 * buf2 <= 160 * 1024 ? 3 : 2;
+        pk = p->rel64 ? k5c2_fn<double>(p->rw, nb2, r) : k5c2_fn<float>(p->rw, nb2, r);
+        if (pk) {
+            p->k5c_r = r;
+            p->k5c_lds = nb2 * buf2;
+            p->k5c_pk = true;
+            OF3D_HIP(hipFuncSetAttribute(pk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
+            p->k5c = pk;
+            return 0;
+        }
+    }
     const size_t buf = (size_t)k5c_groups<F>(p->rw, r) * 1024;
     const int nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;  // two blocks per CU
     const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r) : k5c_fn<F, float>(p->rw, nb, r);
@@ -616,8 +633,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const char* k12_env = getenv("OF3D_K12");
     const int k12_tiles = (int)cdiv(nx, 128 - 2 * p->rd) * (int)cdiv(ny, K12_TY);
     const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
+    // (fp32 plans: K1c + K2c measured faster at c3 / c4 / c5 — 0.41 vs 0.48 ms at c3)
     const void* k12 = (d3 && p->k12 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
-                       (k12_big || (k12_env && k12_env[0] == '1')))
+                       ((k12_big && sizeof(F) == 8) || (k12_env && k12_env[0] == '1')))
                           ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
     // field buffers
     F* D0b = k12 ? Y + 4 * fs : Y;     // temporal derivative (K0 -> K1 / K12), origin zb0
@@ -797,7 +815,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&tp.wr, (void*)&rw_arg, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy,
                             (void*)&ovz, (void*)&orel};
             if (p->k5c) {
-                dim3 gc(cdiv(nx, 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
+                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
                 void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                                  (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz, (void*)&orel};
                 OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, st));
