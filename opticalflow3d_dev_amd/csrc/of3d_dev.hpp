@@ -848,7 +848,12 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
             const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
             if (sg >= nseg) continue;
             F out[RB];
+#ifndef OF3D_EXP_NOB
             lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
+#else  // experiment: phase B without its pass (one LDS read per output)
+#pragma unroll
+            for (int e = 0; e < RB; ++e) out[e] = tile[k34_row(r, cwp) + RW + RB * sg + e];
+#endif
             if (r < nr) {
                 // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
                 const int c0 = RB * sg;
