@@ -43,6 +43,27 @@ const void* k34_fn_uq(int rw, int s) {
     return nullptr;
 }
 
+// Wave-specialised instances (k_prod_wyx_ws: 8 producer + 8 consumer waves, 512 staged
+// columns, 128 VGPRs)
+template <typename F, int NP>
+const void* k34_fn_ws(int rw, int s) {
+    if (const char* e = getenv("OF3D_K34_WS"); e && e[0] == '0') return nullptr;
+#define OF3D_K34W(RW)                                                              \
+    if (rw == RW) {                                                                \
+        if (s == 8) return (const void*)k_prod_wyx_ws<F, NP, RW, 8>;               \
+        if (s == 4) return (const void*)k_prod_wyx_ws<F, NP, RW, 4>;               \
+    }
+    OF3D_K34W(21)
+    OF3D_K34W(15)
+    OF3D_K34W(12)
+#undef OF3D_K34W
+    return nullptr;
+}
+
+template const void* k34_fn_ws<double, 9>(int, int);
+template const void* k34_fn_ws<double, 5>(int, int);
+template const void* k34_fn_ws<float, 9>(int, int);
+template const void* k34_fn_ws<float, 5>(int, int);
 template const void* k34_fn_uq<double, 9>(int, int);
 template const void* k34_fn_uq<double, 5>(int, int);
 template const void* k34_fn_uq<float, 9>(int, int);

@@ -921,6 +921,169 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     }
 }
 
+// K34 with specialised waves (unique staging, 1024 threads): waves 0..7 are producers —
+// phase A (products + W y, one staged column per thread, register ring) writing the W-y
+// tile — and waves 8..15 consumers — phase B (W x + stores) of the PREVIOUS tile, so the
+// producers' gradient loads and the consumers' LDS reads / stores overlap each other's
+// arithmetic instead of alternating in lockstep.  One barrier per tile, two tile buffers:
+// producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
+// k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
+template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2>
+__global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
+                                                      size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
+                                                      int nyb, int cpg, int ngroups) {
+    constexpr int RB = 4, CWA = 512;
+    constexpr int NR = k34_nr(RW, S);
+    constexpr unsigned ES = sizeof(F);
+    static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    F* sw = reinterpret_cast<F*>(smem_raw);  // two W-y tiles [2][S][cwp]
+    const int cwp = k34_pitch(min(tx, nx), RW);
+    const int t = threadIdx.x;
+    const int mb = cpg * NP * nbx;
+    const int kb = blockIdx.x >> 3;
+    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
+    if (g >= ngroups) return;
+    int m = kb % mb;
+    const int bx = m % nbx;
+    m /= nbx;
+    const int p = m % NP, ycl = m / NP;
+    const int nyg = (nyb + cpg - 1) / cpg;
+    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
+    if (yc >= nyb) return;
+    const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
+    const int xo0 = bx * tx;
+    const int txu = min(tx, nx - xo0);
+    const int sxs = max(xo0 - RW, 0);
+    const int ns = min(xo0 + txu + RW, nx) - sxs;
+    const int padL = sxs - (xo0 - RW), padR = (xo0 + txu + RW) - (sxs + ns);
+    const int wa = (ns + 63) >> 6;
+    const bool prod = t < CWA;
+    if (prod && t >= 64 * wa) return;  // producer waves with no staged column leave
+    F h[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k) h[k] = hw[k];
+    const size_t pl = (size_t)zl * ny * nx;
+    const unsigned rowb = (unsigned)nx * ES;
+    const int ntiles = (nrows + S - 1) / S;
+    if (prod) {
+        const unsigned vof = (unsigned)clampi(sxs + t, 0, nx - 1) * ES;
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+        const bool lpad = padL > 0 && wv == 0;
+        const bool rpad = padR > 0 && wv == ((ns - 1) >> 6);
+        const int wpos = t < ns ? padL + t : padL + ns + padR;
+        auto replicas = [&](F* tile) {
+            if (lpad) {
+#pragma unroll
+                for (int r = 0; r < S; ++r) {
+                    F* row = tile + k34_row(r, cwp);
+                    const F e = row[padL];
+                    if (ln < padL) row[ln] = e;
+                }
+            }
+            if (rpad) {
+#pragma unroll
+                for (int r = 0; r < S; ++r) {
+                    F* row = tile + k34_row(r, cwp);
+                    const F e = row[padL + ns - 1];
+                    if (ln < padR) row[padL + ns + ln] = e;
+                }
+            }
+        };
+        constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;
+        constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
+        const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
+        const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
+        auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
+        F ring[NR], ra[PD], rb[PD];
+#pragma unroll
+        for (int i = 0; i <= 2 * RW; ++i) {
+            const unsigned o = rowoff(i);
+            ring[i] = buf_ld<F>(ra_, vof, o) * buf_ld<F>(rb_, vof, o);
+        }
+#pragma unroll
+        for (int i = 0; i < PD; ++i) {
+            const unsigned o = rowoff(2 * RW + 1 + i);
+            ra[(2 * RW + 1 + i) % PD] = buf_ld<F>(ra_, vof, o);
+            rb[(2 * RW + 1 + i) % PD] = buf_ld<F>(rb_, vof, o);
+        }
+        for (int u0 = 0; u0 < nrows; u0 += NR) {
+            bool done = false;
+            [&]<int... H>(std::integer_sequence<int, H...>) {
+                (
+                    [&] {
+                        if (done) return;
+                        constexpr int h0 = H * S;
+                        F* tile = sw + (((u0 + h0) / S) & 1) * k34_tile(S, cwp);
+                        [&]<int... J>(std::integer_sequence<int, J...>) {
+                            (
+                                [&] {
+                                    constexpr int j = h0 + 2 * J;
+                                    constexpr int ic = j + 2 * RW + 1, ic1 = ic + 1;
+                                    ring[ic % NR] = ra[ic % PD] * rb[ic % PD];
+                                    const unsigned o = rowoff(u0 + ic + PD);
+                                    ra[ic % PD] = buf_ld<F>(ra_, vof, o);
+                                    rb[ic % PD] = buf_ld<F>(rb_, vof, o);
+                                    F p1 = ra[ic1 % PD] * rb[ic1 % PD];
+                                    const unsigned o1 = rowoff(u0 + ic1 + PD);
+                                    ra[ic1 % PD] = buf_ld<F>(ra_, vof, o1);
+                                    rb[ic1 % PD] = buf_ld<F>(rb_, vof, o1);
+                                    F a0 = ring[(j + RW) % NR] * h[0];
+                                    F a1 = ring[(j + 1 + RW) % NR] * h[0];
+                                    a0 = a0 + (ring[j % NR] + ring[(j + 2 * RW) % NR]) * h[RW];
+                                    a1 = a1 + (ring[(j + 1) % NR] + ring[(j + 1 + 2 * RW) % NR]) * h[RW];
+                                    ring[ic1 % NR] = p1;
+#pragma unroll
+                                    for (int k = RW - 1; k >= 1; --k) {
+                                        a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
+                                        a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
+                                    }
+                                    tile[k34_row(j % S, cwp) + wpos] = a0;
+                                    tile[k34_row((j + 1) % S, cwp) + wpos] = a1;
+                                }(),
+                                ...);
+                        }(std::make_integer_sequence<int, S / 2>{});
+                        replicas(tile);
+                        lds_barrier();  // tile published; the consumers are done with the other buffer
+                        if (u0 + h0 + S >= nrows) done = true;
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, NR / S>{});
+            if (done) break;
+        }
+    } else {
+        const int tb = t - CWA;
+        const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+        const int nseg = (txu + RB - 1) / RB;
+        constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW;
+        constexpr int RG = S / RPW;
+        const int nsgw = (nseg + SPW - 1) / SPW;
+        for (int tt = 0; tt < ntiles; ++tt) {
+            lds_barrier();  // tile tt written
+            const F* tile = sw + (tt & 1) * k34_tile(S, cwp);
+            const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
+            for (int i = tb; i < 64 * RG * nsgw; i += CWA) {
+                const int l = i & 63, wg = i >> 6;
+                const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
+                const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
+                if (sg >= nseg) continue;
+                F out[RB];
+                lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
+                if (r < nr) {
+                    const int c0 = RB * sg;
+                    const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
+                    if (c0 + RB <= txu) {
+                        buf_st_n<F, RB>(out, rq_, vo, 0);
+                    } else {
+                        for (int e = 0; e < RB; ++e)
+                            if (c0 + e < txu) buf_st<F>(out[e], rq_, vo + e * ES, 0);
+                    }
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K2c: the gradient z pass (calc_flow.py:279-288, axis 0) as a z march: thread = one
 // (y, x) column, lanes along x (coalesced), marching a chunk of zc output planes with a

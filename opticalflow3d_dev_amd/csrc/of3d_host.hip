@@ -72,6 +72,7 @@ struct of3d_plan {
         const void* fn = nullptr;
         int cw = 0, s = 0, tx = 0, nbx = 0;
         size_t lds = 0;
+        int nthr = 0;  // threads per block when not cw (wave-specialised: 2 cw)
     } k34;
     std::vector<K34Geom> k34_cand;  // geometries that keep >= 8 waves per CU (k34_tune picks)
     bool host_ev = false;            // host entry: record into ev[]
@@ -209,7 +210,7 @@ int k34_setup(of3d_plan* p, int np) {
     int best_waves = 0;
     const char* env_nw = getenv("OF3D_K34_NW");  // overrides (experiments)
     const char* env_s = getenv("OF3D_K34_S");
-    const char* env_uq = getenv("OF3D_K34_UQ");  // 0: duplicate staging only, 1: unique only
+    const char* env_uq = getenv("OF3D_K34_UQ");  // 0: duplicate staging only, 1: unique only (2: specialised only)
     auto occupancy = [&](const void* fn, int cw, size_t lds, int& waves) -> int {
         OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int nb = 0;
@@ -264,9 +265,21 @@ int k34_setup(of3d_plan* p, int np) {
                     int waves = 0;
                     if (lds <= 160 * 1024 && !occupancy(fu, cw, lds, waves) && waves >= nw)
                         p->k34_cand.push_back({fu, cw, s, tx, nbx, lds});
+                    // the wave-specialised form of the same geometry (8 producer + 8 consumer waves)
+                    const void* fw = nw == 8 ? (np == 9 ? k34_fn_ws<F, 9>(rw, s) : k34_fn_ws<F, 5>(rw, s)) : nullptr;
+                    int wsw = 0;
+                    if (fw && lds <= 160 * 1024 && !occupancy(fw, 2 * cw, lds, wsw) && wsw >= 2 * nw)
+                        p->k34_cand.push_back({fw, cw, s, tx, nbx, lds, 2 * cw});
                 }
             }
         }
+    }
+    if (env_uq && env_uq[0] == '2') {  // experiments: the wave-specialised candidates only
+        std::vector<of3d_plan::K34Geom> ws;
+        for (const auto& k : p->k34_cand)
+            if (k.nthr) ws.push_back(k);
+        p->k34_cand = ws;
+        p->k34 = ws.empty() ? of3d_plan::K34Geom{} : ws.front();
     }
     if (!p->k34.fn && !p->k34_cand.empty()) p->k34 = p->k34_cand.front();
     for (const auto& k : p->k34_cand)
@@ -335,7 +348,7 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     int tx = k.tx, nbx = k.nbx;
     void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&hw,
                     (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
-    return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.cw), args, k.lds, s);
+    return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);
 }
 
 // K34 autotune at plan creation: every candidate geometry of k34_setup timed on the
@@ -362,7 +375,7 @@ int k34_tune(of3d_plan* p) {
     // choices from run to run (candidates within noise of each other otherwise flip)
     size_t h0 = 0;
     for (size_t i = 0; i < p->k34_cand.size(); ++i)
-        if (p->k34_cand[i].fn == p->k34.fn && p->k34_cand[i].cw == p->k34.cw) h0 = i;
+        if (p->k34_cand[i].fn == p->k34.fn && p->k34_cand[i].cw == p->k34.cw && p->k34_cand[i].nthr == p->k34.nthr) h0 = i;
     std::swap(p->k34_cand[0], p->k34_cand[h0]);
     float best = 1e30f;
     size_t bi = 0;
@@ -383,8 +396,8 @@ int k34_tune(of3d_plan* p) {
     }
     p->k34 = p->k34_cand[bi];
     if (getenv("OF3D_VERBOSE"))
-        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d (%.3f ms)\n", p->k34_cand.size(),
-                p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, best);
+        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d thr=%d (%.3f ms)\n",
+                p->k34_cand.size(), p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, p->k34.nthr, best);
     return 0;
 }
 
