@@ -928,7 +928,13 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // arithmetic instead of alternating in lockstep.  One barrier per tile, two tile buffers:
 // producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
 // k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
-template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2>
+#ifndef OF3D_K34WS_PD
+#define OF3D_K34WS_PD 2
+#endif
+#ifndef OF3D_K34WS_DB
+#define OF3D_K34WS_DB 2
+#endif
+template <typename F, int NP, int RW, int S, int PD = OF3D_K34WS_PD, int DB = OF3D_K34WS_DB>
 __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
                                                       size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
                                                       int nyb, int cpg, int ngroups) {
