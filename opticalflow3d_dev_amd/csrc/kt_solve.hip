@@ -6,9 +6,10 @@ namespace of3dk {
 
 // K5c instances (window radii with a compiled pass; others use k_wz_solve_dma)
 template <typename F, typename RelT>
-const void* k5c_fn(int rw, int nb, int r) {
+const void* k5c_fn(int rw, int nb, int r, int nw) {
 #define OF3D_K5C(RW) \
     case RW:                                                                                            \
+        if (nw == 8) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8, 8> : nullptr;        \
         if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 4> : nullptr;            \
         return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8> : (const void*)k_wz_solve_c<F, RelT, RW, 2, 8>;
     switch (rw) {
@@ -42,9 +43,9 @@ const void* k5c2_fn(int rw, int nb, int r) {
 
 template const void* k5c2_fn<float>(int, int, int);
 template const void* k5c2_fn<double>(int, int, int);
-template const void* k5c_fn<double, float>(int, int, int);
-template const void* k5c_fn<double, double>(int, int, int);
-template const void* k5c_fn<float, float>(int, int, int);
-template const void* k5c_fn<float, double>(int, int, int);
+template const void* k5c_fn<double, float>(int, int, int, int);
+template const void* k5c_fn<double, double>(int, int, int, int);
+template const void* k5c_fn<float, float>(int, int, int, int);
+template const void* k5c_fn<float, double>(int, int, int, int);
 
 }  // namespace of3dk

@@ -1810,12 +1810,12 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
 // block holds ZC = 8 R output planes of 32 columns and its window of ZC + 2RW planes
 // per field takes NB buffers of HG 1-KiB row groups (fp64, RW 15: 24 KiB each).  Two
 // blocks fit a CU: one block's prologue / epilogue overlaps another's passes.
-template <typename F, typename RelT, int RW, int NB, int R>
-__global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c(const F* __restrict__ Q, int zq0, int nz, int ny, int nx,
-                                                    size_t fs, const F* __restrict__ hw, int zo0, int nzo,
-                                                    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
-                                                    RelT* __restrict__ rel) {
-    constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // columns per block, waves, z-groups per wave
+template <typename F, typename RelT, int RW, int NB, int R, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_solve_c(
+    const F* __restrict__ Q, int zq0, int nz, int ny, int nx, size_t fs, const F* __restrict__ hw, int zo0, int nzo,
+    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel) {
+    // NW 8: 128-plane blocks (one per CU), window 1.33x the output planes instead of 1.66x
+    constexpr int CB = 32, LPC = 64 / CB;  // columns per block, z-groups per wave
     constexpr int ZC = NW * LPC * R;                // output planes per block (R planes per z-group)
     constexpr int H = ZC + 2 * RW;                  // window rows (planes)
     constexpr int EPL = 16 / (int)sizeof(F);        // elements per lane per DMA
@@ -1953,11 +1953,11 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float
         }
     }
 }
-constexpr int k5c_zc(int r) { return 8 * r; }  // output planes per K5c block (R planes per z-group)
+constexpr int k5c_zc(int r, int nw = 4) { return 2 * nw * r; }  // output planes per K5c block (R per z-group)
 template <typename F>
-constexpr int k5c_groups(int rw, int r) {
+constexpr int k5c_groups(int rw, int r, int nw = 4) {
     constexpr int rpwi = 64 / (32 / (16 / (int)sizeof(F)));
-    return (k5c_zc(r) + 2 * rw + rpwi - 1) / rpwi;
+    return (k5c_zc(r, nw) + 2 * rw + rpwi - 1) / rpwi;
 }
 
 // ---------------------------------------------------------------------------

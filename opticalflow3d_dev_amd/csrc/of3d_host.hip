@@ -67,6 +67,7 @@ struct of3d_plan {
     size_t k5c_lds = 0;
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
     bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
+    int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -297,6 +298,7 @@ template <typename F>
 int k5c_setup(of3d_plan* p) {
     p->k5c = nullptr;
     p->k5c_pk = false;
+    p->k5c_nw = 4;
     if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
     if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
     const char* er = getenv("OF3D_K5C_R");
@@ -316,10 +318,23 @@ int k5c_setup(of3d_plan* p) {
             return 0;
         }
     }
-    const size_t buf = (size_t)k5c_groups<F>(p->rw, r) * 1024;
-    const int nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;  // two blocks per CU
-    const void* fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r) : k5c_fn<F, float>(p->rw, nb, r);
+    // OF3D_K5C_NW=8: 8-wave blocks of 128 output planes (window 1.33x the outputs instead of
+    // 1.66x; one block per CU) — bit-identical but measured no faster (c3 1.118 vs 1.121 ms,
+    // c4 8.54 vs 7.90, c5 fp32 43.6 vs 40.4): K5c is not bound by its window re-reads
+    const char* enw = getenv("OF3D_K5C_NW");
+    int nw = enw ? atoi(enw) : 4;
+    if (nw != 8) nw = 4;
+    size_t buf = (size_t)k5c_groups<F>(p->rw, r, nw) * 1024;
+    int nb = nw == 8 ? (3 * buf <= 160 * 1024 ? 3 : 0) : (2 * 3 * buf <= 160 * 1024 ? 3 : 2);  // 4 waves: two blocks per CU
+    const void* fn = nb ? (p->rel64 ? k5c_fn<F, double>(p->rw, nb, r, nw) : k5c_fn<F, float>(p->rw, nb, r, nw)) : nullptr;
+    if (!fn && nw == 8) {  // no 8-wave instance: the 4-wave one
+        nw = 4;
+        buf = (size_t)k5c_groups<F>(p->rw, r, nw) * 1024;
+        nb = 2 * 3 * buf <= 160 * 1024 ? 3 : 2;
+        fn = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r, nw) : k5c_fn<F, float>(p->rw, nb, r, nw);
+    }
     if (!fn) return 0;
+    p->k5c_nw = nw;
     p->k5c_r = r;
     p->k5c_lds = nb * buf;
     OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
@@ -828,10 +843,10 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&tp.wr, (void*)&rw_arg, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy,
                             (void*)&ovz, (void*)&orel};
             if (p->k5c) {
-                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), ny, cdiv(no, k5c_zc(p->k5c_r)));
+                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), ny, cdiv(no, k5c_zc(p->k5c_r, p->k5c_nw)));
                 void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
                                  (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz, (void*)&orel};
-                OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(256), cargs, p->k5c_lds, st));
+                OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
             } else if (p->k5_nb) {
                 const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
                 OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5d_lds, st));
@@ -964,10 +979,10 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->device = device;
     if (build_taps(taps, p.get())) return -1;
     OF3D_HIP(hipSetDevice(device));
-    if (set_attrs(p.get())) return -1;
     int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
     p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
     p->fs = (size_t)p->cap_planes * ny * nx;
+    if (set_attrs(p.get())) return -1;
     OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
     OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
     {

@@ -14,7 +14,7 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK", "OF3D_K5C_NW")
 
 
 def _run(img, s, t, w, ndim, mode, old, force=None):
@@ -105,5 +105,19 @@ def test_packed_fp32_wz_solve(case):
     img = np.random.default_rng(500 + case).integers(0, 4096, size=shape).astype(np.uint16)
     new = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=False, force={"OF3D_K5C_PK": "1"})
     ref = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", range(3))
+@pytest.mark.parametrize("fp32", [False, True])
+def test_wz_solve_eight_wave_blocks(case, fp32):
+    """K5c with 8-wave, 128-plane blocks (OF3D_K5C_NW=8; the default for volumes with >= 128
+    output planes) forced on small volumes: bit-identical to the older kernels."""
+    shape, (s, t, w), ndim = CASES[case]
+    img = np.random.default_rng(600 + case).integers(0, 4096, size=shape).astype(np.uint16)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    new = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_K5C_NW": "8"})
+    ref = _run(img, s, t, w, ndim, mode, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
