@@ -351,6 +351,7 @@ def run_slab(args, world, rank, local_rank, dev):
     ai0, ai1 = halo_planes(n_ax, a0, a1, rd, rw) if pworld > 1 else (0, n_ax)
     mode = _lib.OF3D_FP32 if fp32 else 0
     taps = make_taps(s, t, w)
+    rows_direct = False
     if axis == 0:
         plan = _lib.Plan(3, nz, ny, nx, taps, device=dev.index, max_out_planes=max(a1 - a0, 1),
                          timing=max(args.steps, 1), mode=mode)
@@ -358,6 +359,12 @@ def run_slab(args, world, rank, local_rank, dev):
     else:
         plan = _lib.Plan(3, nz, ai1 - ai0, nx, taps, device=dev.index, timing=max(args.steps, 1), mode=mode)
         blk_shape = (nz, ai1 - ai0, nx)
+        rows_direct = os.environ.get("OF3D_BENCH_ROWS", "1") == "1"
+        if rows_direct:
+            try:  # the W kernels write only the own rows (halo rows only in K0 / gradients / W y)
+                plan.set_rows(a0 - ai0, a1 - ai0)
+            except RuntimeError:
+                rows_direct = False
     nblk = int(np.prod(blk_shape))
     seed = 20260206 + (5 if fp32 else 4)
     # 2 rt + 2 slots: the step's exchange goes to the slot the frame before last read
@@ -367,7 +374,7 @@ def run_slab(args, world, rank, local_rank, dev):
             synthetic_slab(1, nz, ny, nx, ai0, ai1, seed + f, dev, out=ring[f:f + 1])
         else:
             synthetic_slab(1, nz, ny, nx, 0, nz, seed + f, dev, out=ring[f:f + 1], rows=(ai0, ai1))
-    n_full = nblk if axis == 1 else (a1 - a0) * ny * nx
+    n_full = (a1 - a0) * (ny * nx if axis == 0 else nz * nx) if (axis == 0 or rows_direct) else nblk
     vt = torch.float32 if fp32 else torch.float64
     outs = [torch.empty(max(n_full, 1), dtype=vt, device=dev) for _ in range(3)]
     rel = torch.empty(max(n_full, 1), dtype=torch.float32, device=dev)

@@ -167,6 +167,14 @@ int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
  * to the serial order.  A per-stage profile (timing mask with several stages)
  * runs serially; with one timed stage its time is summed over the chunks. */
 int of3d_plan_set_overlap(of3d_plan* plan, int64_t chunk_planes);
+
+/* Output rows (3D plans with the fused products/W-xy and W-z kernels): of3d_plan_execute
+ * then writes only rows [y0, y1) of each output plane, as a compact (z_out1-z_out0,
+ * y1-y0, nx) array; the earlier stages still run on every row (the W-y halo).  A row-slab
+ * shard runs its rows + rd + rw halo rows as the plan's volume and keeps its own rows
+ * this way (no reference counterpart: calc_flow.py:512's parallel loop, split by rows).
+ * Fails (non-zero) where those kernels are not in use; (0, ny) restores the default. */
+int of3d_plan_set_rows(of3d_plan* plan, int64_t y0, int64_t y1);
 const char* of3d_stage_name(int i);
 
 /* Copy `bytes` from src to dst on `stream` with a kernel of at most

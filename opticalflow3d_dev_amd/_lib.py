@@ -37,7 +37,7 @@ EXPORTED = (
     "of3d_plan_create", "of3d_plan_destroy", "of3d_plan_workspace_bytes", "of3d_plan_input_range",
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
-    "of3d_plan_set_overlap", "of3d_cache_clear",
+    "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
 )
 
 
@@ -117,6 +117,8 @@ def load():
         lib.of3d_plan_set_timing_mask.restype = ctypes.c_int
         lib.of3d_plan_set_overlap.argtypes = [P, i64]
         lib.of3d_plan_set_overlap.restype = ctypes.c_int
+        lib.of3d_plan_set_rows.argtypes = [P, i64, i64]
+        lib.of3d_plan_set_rows.restype = ctypes.c_int
         d = ctypes.c_double
         lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
         lib.of3d_flow_stats.restype = ctypes.c_int
@@ -216,6 +218,10 @@ class Plan:
         """of3d_plan_set_overlap: z chunks of chunk_planes output planes, gradient stages of the next
         chunk beside the W-xy / W-z / solve stages of this one (0: serial)."""
         check(self.lib.of3d_plan_set_overlap(self.handle, int(chunk_planes)))
+
+    def set_rows(self, y0, y1):
+        """of3d_plan_set_rows: outputs only rows [y0, y1), compact; raises where unsupported."""
+        check(self.lib.of3d_plan_set_rows(self.handle, int(y0), int(y1)))
 
     def set_timing_stages(self, names=None):
         """Time only these stages (None: all); fewer events, less perturbation."""

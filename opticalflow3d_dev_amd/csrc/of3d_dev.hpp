@@ -729,7 +729,8 @@ template <typename F, int NP, int RW, int S, int RB = 4, int OCC = OF3D_K34_OCC,
           bool UQ = false>
 __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
                                                        int nx, size_t fs, const F* __restrict__ hw, int tx,
-                                                       int nyc, int nbx, int nyb, int cpg, int ngroups) {
+                                                       int nyc, int nbx, int nyb, int cpg, int ngroups, int yb0,
+                                                       int yb1) {
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
     constexpr int PD0 = PDX ? PDX : (sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8));
@@ -758,7 +759,8 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const int nyg = (nyb + cpg - 1) / cpg;
     const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
     if (yc >= nyb) return;
-    const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
+    // output rows [yb0, yb1) (row-slab plans: the rank's own rows; loads still clamp at [0, ny))
+    const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
     const int xo0 = bx * tx;
     const int txu = min(tx, nx - xo0);  // useful outputs of this block
     // Staged columns, tile position i <-> column xo0 - RW + i.
@@ -937,7 +939,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 template <typename F, int NP, int RW, int S, int PD = OF3D_K34WS_PD, int DB = OF3D_K34WS_DB>
 __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
                                                       size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
-                                                      int nyb, int cpg, int ngroups) {
+                                                      int nyb, int cpg, int ngroups, int yb0, int yb1) {
     constexpr int RB = 4, CWA = 512;
     constexpr int NR = k34_nr(RW, S);
     constexpr unsigned ES = sizeof(F);
@@ -957,7 +959,8 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
     const int nyg = (nyb + cpg - 1) / cpg;
     const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
     if (yc >= nyb) return;
-    const int y0 = yc * nyc, nrows = min(nyc, ny - y0);
+    // output rows [yb0, yb1) (row-slab plans: the rank's own rows; loads still clamp at [0, ny))
+    const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
     const int xo0 = bx * tx;
     const int txu = min(tx, nx - xo0);
     const int sxs = max(xo0 - RW, 0);
@@ -1813,7 +1816,7 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
 template <typename F, typename RelT, int RW, int NB, int R, int NW = 4>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_solve_c(
     const F* __restrict__ Q, int zq0, int nz, int ny, int nx, size_t fs, const F* __restrict__ hw, int zo0, int nzo,
-    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel) {
+    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel, int yo0) {
     // NW 8: 128-plane blocks (one per CU), window 1.33x the output planes instead of 1.66x
     constexpr int CB = 32, LPC = 64 / CB;  // columns per block, z-groups per wave
     constexpr int ZC = NW * LPC * R;                // output planes per block (R planes per z-group)
@@ -1828,7 +1831,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int col = lane % CB, gz = w * LPC + lane / CB;
     const int x = blockIdx.x * CB + col;
-    const int y = blockIdx.y;
+    const int y = yo0 + blockIdx.y;  // outputs: rows [yo0, yo0 + gridDim.y) in a compact layout
     const int zc0 = zo0 + blockIdx.z * ZC;
     const size_t ps = (size_t)ny * nx;
     const int xc = min((int)blockIdx.x * CB + EPL * (lane % LPR), nx - EPL);  // this lane's DMA columns
@@ -1869,7 +1872,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
     if (x >= nx) return;
-    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
+    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)blockIdx.y * nx + x, (size_t)gridDim.y * nx, vx,
+                               vy, vz, rel);
 }
 // K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
 // float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each
@@ -1882,7 +1886,7 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float
                                                                    int nx, size_t fs, const float* __restrict__ hw,
                                                                    int zo0, int nzo, float* __restrict__ vx,
                                                                    float* __restrict__ vy, float* __restrict__ vz,
-                                                                   RelT* __restrict__ rel) {
+                                                                   RelT* __restrict__ rel, int yo0) {
     using V = f32x2;
     constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // lane-columns (2 columns each), waves, z-groups per wave
     constexpr int ZC = NW * LPC * R;
@@ -1896,7 +1900,7 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int col = lane % CB, gz = w * LPC + lane / CB;
     const int x = blockIdx.x * 2 * CB + 2 * col;  // the lane's first column
-    const int y = blockIdx.y;
+    const int y = yo0 + blockIdx.y;  // outputs: rows [yo0, yo0 + gridDim.y), compact layout
     const int zc0 = zo0 + blockIdx.z * ZC;
     const size_t ps = (size_t)ny * nx;
     const int xc = min((int)blockIdx.x * 2 * CB + 4 * (lane % LPR), nx - 4);  // this lane's DMA floats
@@ -1938,7 +1942,7 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         if (z0l + i >= nzo) break;
-        const size_t o = (size_t)(z0l + i) * ps + (size_t)y * nx + x;
+        const size_t o = (size_t)(z0l + i) * gridDim.y * nx + (size_t)blockIdx.y * nx + x;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
             if (x + e >= nx) break;

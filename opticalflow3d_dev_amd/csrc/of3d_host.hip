@@ -68,6 +68,7 @@ struct of3d_plan {
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
     bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
     int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
+    int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -348,21 +349,23 @@ int k5c_setup(of3d_plan* p) {
 // planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
 template <typename K, typename F>
 hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
-                      hipStream_t s) {
-    const int nyb_max = std::max(1, ny / 32);
+                      hipStream_t s, int yb0 = 0, int yb1 = -1) {
+    if (yb1 < 0) yb1 = ny;
+    const int nyo = yb1 - yb0;  // output rows (row-slab plans: the own rows)
+    const int nyb_max = std::max(1, nyo / 32);
     static const long target = 4L * 256 * 2 * (getenv("OF3D_K34_NYBX") ? atol(getenv("OF3D_K34_NYBX")) : 2);
     int nyb = 1;
     while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
-    int nyc = (ny + nyb - 1) / nyb;
+    int nyc = (nyo + nyb - 1) / nyb;
     nyc = (nyc + k.s - 1) / k.s * k.s;
-    nyb = (ny + nyc - 1) / nyc;
+    nyb = (nyo + nyc - 1) / nyc;
     int cpg = ng >= 32 ? nyb : 1;
     int groups = ng * ((nyb + cpg - 1) / cpg);
     const int mb = cpg * nf * k.nbx;
     const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
     int tx = k.tx, nbx = k.nbx;
-    void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&hw,
-                    (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups};
+    void* args[] = {(void*)&G,   (void*)&P,   (void*)&ny,  (void*)&nx,  (void*)&fs,     (void*)&hw,  (void*)&tx,
+                    (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1};
     return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);
 }
 
@@ -796,7 +799,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         if (q1 <= q0) return 0;
         const int ng = (int)(q1 - q0);
         const size_t o = (size_t)(q0 - R.zg0) * plane;
-        OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st));
+        OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st, (int)p->ya, (int)p->yb));
         return 0;
     };
     auto k3k4 = [&](hipStream_t st) -> int {  // fallback: W y and W x as two kernels (whole range)
@@ -825,7 +828,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     };
     auto k5 = [&](int64_t o0, int64_t o1, int64_t q1, hipStream_t st) -> int {
         if (o1 <= o0) return 0;
-        const size_t oo = (size_t)(o0 - R.zo0) * plane;
+        const size_t oo = (size_t)(o0 - R.zo0) * (size_t)(p->yb - p->ya) * nx;  // output planes: own rows
         F* ovx = vx + oo;
         F* ovy = vy + oo;
         F* ovz = d3 ? vz + oo : nullptr;
@@ -843,9 +846,11 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&tp.wr, (void*)&rw_arg, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy,
                             (void*)&ovz, (void*)&orel};
             if (p->k5c) {
-                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), ny, cdiv(no, k5c_zc(p->k5c_r, p->k5c_nw)));
-                void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w,
-                                 (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz, (void*)&orel};
+                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), (unsigned)(p->yb - p->ya), cdiv(no, k5c_zc(p->k5c_r, p->k5c_nw)));
+                int yo0 = (int)p->ya;
+                void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny,  (void*)&nx,  (void*)&fs,
+                                 (void*)&tp.w, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz,
+                                 (void*)&orel, (void*)&yo0};
                 OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
             } else if (p->k5_nb) {
                 const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
@@ -976,6 +981,8 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->nz = nz;
     p->ny = ny;
     p->nx = nx;
+    p->ya = 0;
+    p->yb = ny;
     p->device = device;
     if (build_taps(taps, p.get())) return -1;
     OF3D_HIP(hipSetDevice(device));
@@ -1310,6 +1317,18 @@ int of3d_plan_stage_times(of3d_plan* p, double* ms, int cap) {
     if (p->k34.fn && m > 3) ms[3] = -1.0;  // fused K34: "prod_wy" holds W x too, "wx" is empty
     p->tcount = 0;
     return m;
+}
+
+int of3d_plan_set_rows(of3d_plan* p, int64_t y0, int64_t y1) {
+    if (!p) return fail("of3d: null plan");
+    if (y0 < 0 || y1 > p->ny || y0 >= y1) return fail("of3d: bad output row range");
+    if (y0 != 0 || y1 != p->ny) {
+        if (p->ndim != 3 || p->general || !p->k34.fn || !p->k5c || p->zchunk > 0)
+            return fail("of3d: output row ranges need the fused K34 and K5c kernels (3D, serial)");
+    }
+    p->ya = y0;
+    p->yb = y1;
+    return 0;
 }
 
 int of3d_plan_set_overlap(of3d_plan* p, int64_t chunk_planes) {

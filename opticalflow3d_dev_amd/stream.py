@@ -92,6 +92,7 @@ class FlowStream:
         self.plan = None
         self.z0, self.z1, self.zi0, self.zi1 = 0, nz, 0, nz
         self.y0, self.y1, self.yi0, self.yi1 = 0, ny, 0, ny
+        self.rows_direct = False
         if self.axis == 0:
             self.z0, self.z1 = zslab_bounds(nz, self.rank, self.world)
             if zslab is not None:
@@ -112,8 +113,14 @@ class FlowStream:
             self.nvox = nz * (self.y1 - self.y0) * nx
             self.nblock = nz * (self.yi1 - self.yi0) * nx
             self.own0 = 0
+            self.rows_direct = False  # the plan writes only the own rows (of3d_plan_set_rows)
             if self.nvox > 0:
                 self.plan = _lib.Plan(3, nz, self.yi1 - self.yi0, nx, taps, device=self.device, mode=mode)
+                try:
+                    self.plan.set_rows(self.y0 - self.yi0, self.y1 - self.yi0)
+                    self.rows_direct = True
+                except RuntimeError:  # kernels without row ranges: whole sub-volume, then a slice
+                    pass
         # nwin + 1 slots: a new frame's upload (and halo exchange) goes to the slot the
         # frame before last read, so it overlaps the previous frame's compute
         self.ring = torch.empty((self.nwin + 1, max(self.nblock, 1)), dtype=tdt, device=self.dev)
@@ -161,8 +168,9 @@ class FlowStream:
                                [torch.empty(n, dtype=rel_t, device=None if pin else self.dev, pin_memory=pin)]
         self.dout = [mk(False) for _ in range(depth)]
         self.hout = [mk(True) for _ in range(depth)]
-        # row slabs: the plan writes all rows of its sub-volume here; the own rows are copied out
-        self.dfull = mk(False, max(self.nblock, 1)) if self.axis == 1 else None
+        # row slabs without row ranges: the plan writes all rows of its sub-volume here; the own
+        # rows are copied out
+        self.dfull = mk(False, max(self.nblock, 1)) if self.axis == 1 and not self.rows_direct else None
         self.host_free = [threading.Event() for _ in range(depth)]  # set: writer released the set
         for e in self.host_free:
             e.set()
@@ -236,6 +244,9 @@ class FlowStream:
         if self.plan is not None and self.axis == 0:
             self.plan.execute(ptrs, self.code, self.zi0, self.z0, self.z1 if self.ndim == 3 else 1,
                               dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
+        elif self.plan is not None and self.rows_direct:  # row slab: the plan writes the own rows
+            self.plan.execute(ptrs, self.code, 0, 0, self.nz, dout[0].data_ptr(), dout[1].data_ptr(),
+                              dout[2].data_ptr(), dout[-1].data_ptr(), self.comp.cuda_stream)
         elif self.plan is not None:  # row slab: whole sub-volume, then the own rows
             full = self.dfull
             self.plan.execute(ptrs, self.code, 0, 0, self.nz, full[0].data_ptr(), full[1].data_ptr(),

@@ -94,6 +94,25 @@ def test_sequencet_zslab_three_ranks(tmp_path):
         assert_flow3d_matches_oracle(got, stack[hh:hh + 7], 1, 1, 2)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_yslab_row_ranges_wsig5(tmp_path, world):
+    """Row slabs where the fused W kernels are in use (wSig 5: rw 15), so every rank's plan
+    writes only its own rows (of3d_plan_set_rows): files equal one GPU's, pixels the oracle's."""
+    stack = np.random.default_rng(10 + world).integers(0, 4096, size=(7, 3, 96, 40)).astype(np.uint16)
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    for d in (single, multi):
+        d.mkdir()
+        tf.imwrite(d / "w.tif", stack, imagej=True)
+    process_flow(str(single), "w", "OneTif", 3, 1, 1, 5)
+    _run_ranks(world, (str(multi), "w", "OneTif", 3, 1, 1, 5), {"parallel": "yslab"})
+    a, b = _tree(single / "OpticalFlow3D"), _tree(multi / "OpticalFlow3D")
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k] == b[k], k
+    got = [tf.imread(multi / "OpticalFlow3D" / "w" / f"w_{n}_t0003.tiff") for n in ("vx", "vy", "vz", "rel")]
+    assert_flow3d_matches_oracle(got, stack, 1, 1, 5)
+
+
 def test_sequencet_yslab_two_ranks(tmp_path):
     stack = np.random.default_rng(8).integers(0, 4096, size=(7, 4, 36, 18)).astype(np.uint16)
     for t in range(7):

@@ -88,3 +88,40 @@ def test_zslab_ranks_with_halo_exchange(world):
         for a, b in zip(full, outs):
             assert bits_equal(a[z0:z1], b.reshape(z1 - z0, 20, 24))
     assert covered == 30
+
+
+@pytest.mark.parametrize("rows", [(0, 60), (7, 41), (0, 1), (59, 60), (13, 14)])
+@pytest.mark.parametrize("fp32", [False, True])
+def test_plan_output_rows(rows, fp32):
+    """of3d_plan_set_rows: the fused W kernels write only rows [y0, y1) (compact), bit-identical
+    to the same rows of the whole-plane outputs (row slabs keep their own rows this way)."""
+    import torch
+
+    ya, yb = rows
+    img = np.random.default_rng(11).integers(0, 4096, size=(13, 20, 60, 40)).astype(np.uint16)
+    s, t, w = 2, 2, 5
+    rt = radii(s, t, w)[2]
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(np.ascontiguousarray(img[6 - rt:6 + rt + 1]).view(np.int16)).to(dev)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    vt = torch.float32 if fp32 else torch.float64
+
+    def run(r0, r1):
+        plan = _lib.Plan(3, 20, 60, 40, make_taps(s, t, w), device=0, mode=mode)
+        try:
+            if (r0, r1) != (0, 60):
+                plan.set_rows(r0, r1)
+            n = 20 * (r1 - r0) * 40
+            outs = [torch.empty(n, dtype=vt, device=dev) for _ in range(3)] + [torch.empty(n, dtype=torch.float32,
+                                                                                          device=dev)]
+            plan.execute([d_in[i].data_ptr() for i in range(2 * rt + 1)], _lib.OF3D_U16, 0, 0, 20,
+                         *[o.data_ptr() for o in outs])
+            torch.cuda.synchronize(dev)
+            return [o.cpu().numpy().reshape(20, r1 - r0, 40) for o in outs]
+        finally:
+            plan.close()
+
+    full = run(0, 60)
+    part = run(ya, yb)
+    for a, b in zip(full, part):
+        assert np.array_equal(a[:, ya:yb].view(np.uint8), b.view(np.uint8))
