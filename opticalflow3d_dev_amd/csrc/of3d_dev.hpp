@@ -1865,15 +1865,35 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
+#ifndef OF3D_EXP_K5_NOPASS
         lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
+#else  // experiment: no W-z arithmetic (one LDS read per output)
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[f][i] = sm[(f % NB) * HG * RPWI * CB + col + (RW + gz * R + i) * CB];
+#endif
         // pin the pass here: without it the compiler sinks every field's arithmetic below the
         // last barrier and keeps all 9 windows' LDS reads live in registers (spills)
 #pragma unroll
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
     if (x >= nx) return;
+#ifndef OF3D_EXP_K5_NOSOLVE
     k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)blockIdx.y * nx + x, (size_t)gridDim.y * nx, vx,
                                vy, vz, rel);
+#else  // experiment: no solve / eigenvalue (stores the field sums)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        if (zc0 + gz * R - zo0 + i >= nzo) break;
+        F a = acc[0][i];
+#pragma unroll
+        for (int f = 1; f < 9; ++f) a = a + acc[f][i];
+        const size_t o = (size_t)(zc0 + gz * R - zo0 + i) * gridDim.y * nx + (size_t)blockIdx.y * nx + x;
+        vx[o] = a;
+        vy[o] = a;
+        vz[o] = a;
+        rel[o] = (RelT)a;
+    }
+#endif
 }
 // K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
 // float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each
