@@ -175,6 +175,12 @@ int of3d_plan_set_overlap(of3d_plan* plan, int64_t chunk_planes);
  * this way (no reference counterpart: calc_flow.py:512's parallel loop, split by rows).
  * Fails (non-zero) where those kernels are not in use; (0, ny) restores the default. */
 int of3d_plan_set_rows(of3d_plan* plan, int64_t y0, int64_t y1);
+
+/* Kernel families this plan has launched so far, comma-separated (e.g.
+ * "k_tderiv_c,k_grad_xyz_c,k_prod_wyx_ws,k_wz_solve_c"), written NUL-terminated into
+ * buf (at most n bytes); returns the full length.  Diagnostics: which kernels a
+ * parameter set / volume shape runs on (no reference counterpart). */
+int of3d_plan_kernels(const of3d_plan* plan, char* buf, size_t n);
 const char* of3d_stage_name(int i);
 
 /* Copy `bytes` from src to dst on `stream` with a kernel of at most

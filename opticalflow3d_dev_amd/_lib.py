@@ -38,6 +38,7 @@ EXPORTED = (
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
+    "of3d_plan_kernels",
 )
 
 
@@ -119,6 +120,8 @@ def load():
         lib.of3d_plan_set_overlap.restype = ctypes.c_int
         lib.of3d_plan_set_rows.argtypes = [P, i64, i64]
         lib.of3d_plan_set_rows.restype = ctypes.c_int
+        lib.of3d_plan_kernels.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
+        lib.of3d_plan_kernels.restype = ctypes.c_int
         d = ctypes.c_double
         lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
         lib.of3d_flow_stats.restype = ctypes.c_int
@@ -222,6 +225,13 @@ class Plan:
     def set_rows(self, y0, y1):
         """of3d_plan_set_rows: outputs only rows [y0, y1), compact; raises where unsupported."""
         check(self.lib.of3d_plan_set_rows(self.handle, int(y0), int(y1)))
+
+    def kernels(self):
+        """of3d_plan_kernels: the kernel families this plan has launched so far."""
+        n = check(self.lib.of3d_plan_kernels(self.handle, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        check(self.lib.of3d_plan_kernels(self.handle, buf, n + 1))
+        return [k for k in buf.value.decode().split(",") if k]
 
     def set_timing_stages(self, names=None):
         """Time only these stages (None: all); fewer events, less perturbation."""

@@ -4,7 +4,7 @@
 
 namespace of3dk {
 
-// K34 instances: W radii with a compiled register ring (others use K3 + K4)
+// K34 instances: W radii with a compiled register ring, wSig 3..7 (others use K3 + K4)
 template <typename F, int NP>
 const void* k34_fn(int rw, int s, int rb) {
 #define OF3D_K34(RW, SA, SB)                                    \
@@ -13,12 +13,11 @@ const void* k34_fn(int rw, int s, int rb) {
         if (s == SB) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, RW, SB>;                                     \
         return nullptr;
     switch (rw) {
+        OF3D_K34(9, 16, 8)
         OF3D_K34(12, 16, 8)
         OF3D_K34(15, 16, 8)
-    case 21:  // register ring of 44-48 rows: shorter tiles
-        if (s == 8) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, 21, 8>;
-        if (s == 4) return rb == 2 ? nullptr : (const void*)k_prod_wyx<F, NP, 21, 4>;
-        return nullptr;
+        OF3D_K34(18, 8, 4)  // register ring of 38-48 rows: shorter tiles
+        OF3D_K34(21, 8, 4)
         default: return nullptr;
     }
 #undef OF3D_K34
@@ -37,8 +36,10 @@ const void* k34_fn_uq(int rw, int s) {
         if (s == 4) return (const void*)k_prod_wyx<F, NP, RW, 4, 4, 2, 4, 2, true>;        \
     }
     OF3D_K34U(21)
+    OF3D_K34U(18)
     OF3D_K34U(15)
     OF3D_K34U(12)
+    OF3D_K34U(9)
 #undef OF3D_K34U
     return nullptr;
 }
@@ -54,8 +55,10 @@ const void* k34_fn_ws(int rw, int s) {
         if (s == 4) return (const void*)k_prod_wyx_ws<F, NP, RW, 4>;               \
     }
     OF3D_K34W(21)
+    OF3D_K34W(18)
     OF3D_K34W(15)
     OF3D_K34W(12)
+    OF3D_K34W(9)
 #undef OF3D_K34W
     return nullptr;
 }

@@ -4,7 +4,7 @@
 
 namespace of3dk {
 
-// K5c instances (window radii with a compiled pass; others use k_wz_solve_dma)
+// K5c instances (window radii with a compiled pass, wSig 3..7; others use k_wz_solve_dma)
 template <typename F, typename RelT>
 const void* k5c_fn(int rw, int nb, int r, int nw) {
 #define OF3D_K5C(RW) \
@@ -13,8 +13,10 @@ const void* k5c_fn(int rw, int nb, int r, int nw) {
         if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 4> : nullptr;            \
         return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8> : (const void*)k_wz_solve_c<F, RelT, RW, 2, 8>;
     switch (rw) {
+        OF3D_K5C(9)
         OF3D_K5C(12)
         OF3D_K5C(15)
+        OF3D_K5C(18)
         OF3D_K5C(21)
         default: return nullptr;
     }
@@ -33,8 +35,10 @@ const void* k5c2_fn(int rw, int nb, int r) {
         if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c2<RelT, RW, 3, 4> : nullptr;              \
         return nb == 3 ? (const void*)k_wz_solve_c2<RelT, RW, 3, 8> : (const void*)k_wz_solve_c2<RelT, RW, 2, 8>;
     switch (rw) {
+        OF3D_K5C2(9)
         OF3D_K5C2(12)
         OF3D_K5C2(15)
+        OF3D_K5C2(18)
         OF3D_K5C2(21)
         default: return nullptr;
     }

@@ -40,6 +40,17 @@ constexpr int kMaxChunks = 16;  // overlap mode: most z chunks per execution
 
 }  // namespace
 
+// kernel families (of3d_plan_kernels)
+enum : unsigned {
+    KU_K0C = 1u << 0, KU_K0 = 1u << 1, KU_K1C = 1u << 2, KU_K1 = 1u << 3, KU_K12 = 1u << 4, KU_K2C = 1u << 5,
+    KU_K2 = 1u << 6, KU_K34 = 1u << 7, KU_K34WS = 1u << 8, KU_K3 = 1u << 9, KU_K4 = 1u << 10, KU_K5C = 1u << 11,
+    KU_K5C_PK = 1u << 12, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
+};
+constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy_c",    "k_grad_xy",  "k_grad_xyz_c",
+                                        "k_grad_z_c", "k_grad_z",     "k_prod_wyx",     "k_prod_wyx_ws", "k_prod_wy",
+                                        "k_wx",       "k_wz_solve_c", "k_wz_solve_c2",  "k_wz_solve_dma", "k_wz_solve",
+                                        "k_solve2d",  "general"};
+
 struct of3d_plan {
     int ndim = 3;
     bool rel64 = false;  // OF3D_REL_F64
@@ -69,6 +80,7 @@ struct of3d_plan {
     bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
     int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
     int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
+    unsigned used = 0;       // kernel families launched so far (KU_* bits, of3d_plan_kernels)
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -701,14 +713,17 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             if (k0) {
                 void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
                 OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, st));
+                p->used |= KU_K0C;
             } else {
                 OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
+                p->used |= KU_K0;
             }
         } else {
             const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
             void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
                             (void*)&D0};
             OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
+            p->used |= KU_K0;
         }
         if (k12) return 0;  // the y / x passes run inside K12 (stage grad_z)
         const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
@@ -739,8 +754,10 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             void* cargs[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&tp, (void*)&Bo,
                              (void*)&fs, (void*)&need_b4, (void*)&tx, (void*)&nyc, (void*)&nbx, (void*)&nyb};
             OF3D_HIP(hipLaunchKernel(k1c, dim3(blocks), dim3(cw), cargs, lds, st));
+            p->used |= KU_K1C;
         } else {
             OF3D_HIP(hipLaunchKernel(k1_kernel_dt<F>(dtype, p->rd), g, dim3(64, 4), args, p->k1_lds, st));
+            p->used |= KU_K1;
         }
         return 0;
     };
@@ -769,6 +786,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&Go, (void*)&fs, (void*)&zg0, (void*)&qa, (void*)&nq, (void*)&zc, (void*)&ntile,
                             (void*)&nbx};
             OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(128 * K12_TY), args, lds, st));
+            p->used |= KU_K12;
             return 0;
         }
         const void* k2c = nullptr;
@@ -788,10 +806,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             void* args[] = {(void*)&Bc, (void*)&zb0, (void*)&Go, (void*)&zg0, (void*)&ngz, (void*)&nzz, (void*)&pl,
                             (void*)&fs, (void*)&tp, (void*)&zc};
             OF3D_HIP(hipLaunchKernel(k2c, dim3(cdiv(pl, 256), cdiv(ng, zc)), dim3(256), args, 0, st));
+            p->used |= KU_K2C;
         } else {
             dim3 g(cdiv(nx, 64), ny, cdiv(ng, K2_ZC) * 4);
             hipLaunchKernelGGL(k_grad_z<F>, g, dim3(64, 4), p->k2_lds, st, Bc, zb0, Go, zg0, ngz, nzz, ny, nx, fs, tp);
             OF3D_HIP(hipGetLastError());
+            p->used |= KU_K2;
         }
         return 0;
     };
@@ -800,6 +820,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         const int ng = (int)(q1 - q0);
         const size_t o = (size_t)(q0 - R.zg0) * plane;
         OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st, (int)p->ya, (int)p->yb));
+        p->used |= p->k34.nthr ? KU_K34WS : KU_K34;
         return 0;
     };
     auto k3k4 = [&](hipStream_t st) -> int {  // fallback: W y and W x as two kernels (whole range)
@@ -812,6 +833,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             void* args[] = {(void*)&G, (void*)&P, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
                             (void*)&rw_arg};
             OF3D_HIP(hipLaunchKernel(k3_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k3_lds, st));
+            p->used |= KU_K3;
         }
         return 0;
     };
@@ -824,6 +846,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         void* args[] = {(void*)&Pc, (void*)&Q, (void*)&ny, (void*)&nx, (void*)&fs, (void*)&tp.w, (void*)&tp.wr,
                         (void*)&rw_arg};
         OF3D_HIP(hipLaunchKernel(k4_kernel<F>(nf, p->rw), g, dim3(64, 4), args, p->k4_lds, st));
+        p->used |= KU_K4;
         return 0;
     };
     auto k5 = [&](int64_t o0, int64_t o1, int64_t q1, hipStream_t st) -> int {
@@ -852,16 +875,20 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                                  (void*)&tp.w, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz,
                                  (void*)&orel, (void*)&yo0};
                 OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
+                p->used |= p->k5c_pk ? KU_K5C_PK : KU_K5C;
             } else if (p->k5_nb) {
                 const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
                 OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5d_lds, st));
+                p->used |= KU_K5DMA;
             } else {
                 const void* k = p->rel64 ? k5_kernel<F, double>(p->rw) : k5_kernel<F, float>(p->rw);
                 OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5_lds, st));
+                p->used |= KU_K5;
             }
         } else {
             const int n = ny * nx;
             hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st, (const F*)Qb, fs, n, vx, vy, (F*)rel);
+            p->used |= KU_SOLVE2D;
         }
         OF3D_HIP(hipGetLastError());
         return 0;
@@ -872,6 +899,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     hipEvent_t* evs = p->host_ev ? p->ev : (p->timing_slots ? &p->tev[(size_t)slot * p->tev_per_slot] : nullptr);
     const unsigned tmask = p->host_ev ? (1u << kStages) - 1 : p->timing_mask;
     if (p->general) {
+        p->used |= KU_GENERAL;
         const unsigned bmask = tmask | (tmask << 1);
         auto mark = [&](int i) -> int {
             if (evs && ((bmask >> i) & 1u)) OF3D_HIP(hipEventRecord(evs[i], s));
@@ -1329,6 +1357,19 @@ int of3d_plan_set_rows(of3d_plan* p, int64_t y0, int64_t y1) {
     p->ya = y0;
     p->yb = y1;
     return 0;
+}
+
+int of3d_plan_kernels(const of3d_plan* p, char* buf, size_t n) {
+    if (!p) return fail("of3d: null plan");
+    std::string out;
+    for (size_t i = 0; i < sizeof(kKernelNames) / sizeof(kKernelNames[0]); ++i)
+        if ((p->used >> i) & 1u) out += (out.empty() ? "" : ",") + std::string(kKernelNames[i]);
+    if (buf && n) {
+        const size_t k = std::min(n - 1, out.size());
+        memcpy(buf, out.data(), k);
+        buf[k] = 0;
+    }
+    return (int)out.size();
 }
 
 int of3d_plan_set_overlap(of3d_plan* p, int64_t chunk_planes) {

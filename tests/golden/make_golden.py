@@ -66,6 +66,9 @@ CASES_3D = [
     ("c3d_big_wsig17", lambda: rand_u16((7, 5, 24, 26), 14), (1, 1, 17)),
     # the published benchmark's parameters (PFS/plot_figureS4_computation.ipynb) at Nz = 4
     ("c3d_pub_s3t1w4_nz4", lambda: rand_u16((7, 4, 40, 48), 15), (3, 1, 4)),
+    # W radii 9 and 18 (wSig 3, 6): the fused K34 / K5c instances added for them
+    ("c3d_wsig3", lambda: rand_u16((7, 6, 36, 40), 16), (2, 1, 3)),
+    ("c3d_wsig6", lambda: rand_u16((7, 9, 44, 48), 17), (1, 1, 6)),
 ]
 
 CASES_2D = [

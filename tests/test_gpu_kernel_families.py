@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK", "OF3D_K5C_NW")
 
 
-def _run(img, s, t, w, ndim, mode, old, force=None):
+def _run(img, s, t, w, ndim, mode, old, force=None, kernels=None):
     import torch
 
     saved = {k: os.environ.get(k) for k in FAMILY_ENV}
@@ -47,6 +47,8 @@ def _run(img, s, t, w, ndim, mode, old, force=None):
             plan.execute([d_in[i].data_ptr() for i in range(2 * rt + 1)], _lib.OF3D_U16, 0, 0, nz,
                          outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(), rel.data_ptr())
             torch.cuda.synchronize(dev)
+            if kernels is not None:
+                kernels.extend(plan.kernels())
         finally:
             plan.close()
         res = [o.cpu().numpy() for o in outs[:3 if ndim == 3 else 2]] + [rel.cpu().numpy()]
@@ -119,5 +121,35 @@ def test_wz_solve_eight_wave_blocks(case, fp32):
     mode = _lib.OF3D_FP32 if fp32 else 0
     new = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_K5C_NW": "8"})
     ref = _run(img, s, t, w, ndim, mode, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+W_RADII = [
+    ((7, 10, 90, 200), (2, 1, 3), 3),     # rw 9
+    ((13, 12, 100, 268), (1, 2, 6), 3),   # rw 18 (fp32 K5c: nx % 4 == 0)
+    ((7, 1, 300, 140), (2, 1, 3), 2),     # 2D, rw 9
+    ((7, 1, 240, 300), (1, 1, 6), 2),     # 2D, rw 18
+]
+
+
+@pytest.mark.parametrize("case", range(len(W_RADII)))
+@pytest.mark.parametrize("fp32", [False, True])
+def test_fused_w_kernels_wsig3_wsig6(case, fp32):
+    """wSig 3 and 6 (W radii 9, 18) run the fused K34 / K5c instances (of3d_plan_kernels
+    says so) and agree bit for bit with the separate-pass kernels."""
+    shape, (s, t, w), ndim = W_RADII[case]
+    img = np.random.default_rng(700 + case).integers(0, 4096, size=shape).astype(np.uint16)
+    if ndim == 2:
+        img = img[:, 0]
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    used = []
+    new = _run(img, s, t, w, ndim, mode, old=False, kernels=used)
+    assert any(k.startswith("k_prod_wyx") for k in used), used
+    if ndim == 3:
+        assert any(k.startswith("k_wz_solve_c") for k in used), used
+    old_used = []
+    ref = _run(img, s, t, w, ndim, mode, old=True, kernels=old_used)
+    assert not any(k.startswith("k_prod_wyx") for k in old_used), old_used
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))

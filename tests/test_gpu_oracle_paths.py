@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 ZSLAB_GOLDEN = ["c3d_rand_c2params", "c3d_rand_c3params", "c3d_nz1", "c3d_nz2", "c3d_nz3", "c3d_nz4",
                 "c3d_default_params", "c3d_smooth_translate", "c3d_frac_sigmas", "c3d_big_wsig17",
-                "c3d_pub_s3t1w4_nz4"]
+                "c3d_pub_s3t1w4_nz4", "c3d_wsig3", "c3d_wsig6"]
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -122,7 +122,7 @@ def _smooth(shape, seed):
 
 @pytest.mark.parametrize("name", ["c3d_smooth_translate", "c3d_float32_nt11", "c3d_rand_c2params",
                                   "c3d_rand_c3params", "c3d_default_params", "c3d_flat", "c3d_big_xyzsig9",
-                                  "c3d_big_wsig17", "c3d_pub_s3t1w4_nz4"])
+                                  "c3d_big_wsig17", "c3d_pub_s3t1w4_nz4", "c3d_wsig3", "c3d_wsig6"])
 def test_fp32_3d_vs_golden(name):
     g = load_golden(name)
     got = calc_flow3D_fp32(g["images"], g["sig"], g["tsig"], g["wsig"])
