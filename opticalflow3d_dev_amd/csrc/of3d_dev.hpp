@@ -930,6 +930,8 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // arithmetic instead of alternating in lockstep.  One barrier per tile, two tile buffers:
 // producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
 // k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
+// (12-wave blocks — 4 consumer waves, 168 VGPRs, deeper prefetch, 8-row tiles — measured
+// slower: c3 1.95 vs 1.72 ms, c2 0.27 vs 0.19: the 16-wave occupancy hides more.)
 #ifndef OF3D_K34WS_PD
 #define OF3D_K34WS_PD 2
 #endif
@@ -1375,9 +1377,16 @@ __host__ __device__ constexpr int k12_slot_bytes() { return ((k12_slot_granules<
 constexpr int K12_AP = 132;
 template <typename F>
 __host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * K12_AP * (int)sizeof(F); }
-// planes per DMA chunk: 3 where two chunks of slots + the A tiles fit 160 KiB, else 2
+// planes per DMA chunk: 2 where two chunks of slots + the A tiles fit 80 KiB and the
+// kernel's registers allow 4 waves per SIMD (fp32 rd 3 / 6: two 8-wave blocks per CU),
+// else 3 where they fit 160 KiB, else 2
+#ifndef OF3D_K12_TWO
+#define OF3D_K12_TWO 1
+#endif
 template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_k() {
+    if (OF3D_K12_TWO && sizeof(F) == 4 && RD <= 6 && 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 80 * 1024)
+        return 2;
     return 6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 3 : 2;
 }
 template <typename T, typename F, int RD>

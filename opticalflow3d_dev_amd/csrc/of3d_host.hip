@@ -676,9 +676,10 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const char* k12_env = getenv("OF3D_K12");
     const int k12_tiles = (int)cdiv(nx, 128 - 2 * p->rd) * (int)cdiv(ny, K12_TY);
     const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
-    // (fp32 plans: K1c + K2c measured faster at c3 / c4 / c5 — 0.41 vs 0.48 ms at c3)
+    // (fp32 plans, rd <= 6: two blocks per CU — c3 0.27 + 0.36 ms vs K1c + K2c 0.43 + 0.25, c5
+    // 12.7 + 21.3 vs 23.5 + 13.2; rd 9 in fp32 runs one block per CU: K1c + K2c)
     const void* k12 = (d3 && p->k12 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
-                       ((k12_big && sizeof(F) == 8) || (k12_env && k12_env[0] == '1')))
+                       ((k12_big && (sizeof(F) == 8 || p->rd <= 6)) || (k12_env && k12_env[0] == '1')))
                           ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
     // field buffers
     F* D0b = k12 ? Y + 4 * fs : Y;     // temporal derivative (K0 -> K1 / K12), origin zb0
