@@ -63,6 +63,26 @@ const void* k34_fn_ws(int rw, int s) {
     return nullptr;
 }
 
+// Packed-fp32 instances (k_prod_wyx_pk: 4 producer + 4 consumer waves on float2 lanes)
+template <int NP>
+const void* k34_fn_pk(int rw, int s) {
+    if (const char* e = getenv("OF3D_K34_PK"); e && e[0] == '0') return nullptr;
+#define OF3D_K34P(RW)                                                      \
+    if (rw == RW) {                                                        \
+        if (s == 8) return (const void*)k_prod_wyx_pk<NP, RW, 8>;          \
+        if (s == 4) return (const void*)k_prod_wyx_pk<NP, RW, 4>;          \
+    }
+    OF3D_K34P(21)
+    OF3D_K34P(18)
+    OF3D_K34P(15)
+    OF3D_K34P(12)
+    OF3D_K34P(9)
+#undef OF3D_K34P
+    return nullptr;
+}
+template const void* k34_fn_pk<9>(int, int);
+template const void* k34_fn_pk<5>(int, int);
+
 template const void* k34_fn_ws<double, 9>(int, int);
 template const void* k34_fn_ws<double, 5>(int, int);
 template const void* k34_fn_ws<float, 9>(int, int);

@@ -970,7 +970,12 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
     const int padL = sxs - (xo0 - RW), padR = (xo0 + txu + RW) - (sxs + ns);
     const int wa = (ns + 63) >> 6;
     const bool prod = t < CWA;
-    if (prod && t >= 64 * wa) return;  // producer waves with no staged column leave
+    // producer waves with no staged column: every wave still takes one barrier per tile
+    // (a wave-uniform test, so the whole wave takes this branch)
+    if (prod && __builtin_amdgcn_readfirstlane(t >> 6) >= wa) {
+        for (int tt = 0; tt < (nrows + S - 1) / S; ++tt) lds_barrier();
+        return;
+    }
     F h[RW + 1];
 #pragma unroll
     for (int k = 0; k <= RW; ++k) h[k] = hw[k];
@@ -1091,6 +1096,206 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                     }
                 }
             }
+        }
+    }
+}
+
+// Packed-fp32 K34 (OF3D_FP32 plans): k_prod_wyx_ws's producer / consumer split on CDNA's
+// packed fp32 math (v_pk_mul_f32 / v_pk_add_f32: two lanes of work per instruction, each
+// element rounded as the scalar op — bit-identical to the fp32 kernels).  8-wave blocks
+// (two per CU): waves 0..3 producers, one PAIR of staged columns per thread (512 staged
+// columns), phase A on float2 {column c, c + 1}; waves 4..7 consumers, phase B on float2
+// {row 2p, row 2p + 1}.  The W-y tile is stored row-pair interleaved — tile2[p][x] =
+// {W-y(2p, x), W-y(2p + 1, x)} — so both phases read and write aligned float2: the
+// producer's two rows j, j + 1 of columns c, c + 1 are the pair row j / 2 at x = c, c + 1.
+// Pair pitch P2 = 1 (mod 32) float2: the consumers' 4 pairs x 4 segments of a 16-lane
+// group hit 32 distinct banks.  Ring, prefetch and tile double-buffering as k_prod_wyx_ws.
+template <int NP, int RW, int S, int PD = 2, int DB = 2>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_prod_wyx_pk(const float* __restrict__ G, float* __restrict__ Q, int ny,
+                                                     int nx, size_t fs, const float* __restrict__ hw, int tx,
+                                                     int nyc, int nbx, int nyb, int cpg, int ngroups, int yb0,
+                                                     int yb1) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    constexpr int RB = 4, NPT = 256;  // outputs per consumer item; producer (= consumer) threads
+    constexpr int NR = k34_nr(RW, S);
+    static_assert(NR % PD == 0 && NR % S == 0 && S % 2 == 0 && (S == 8 || S == 4), "ring sizes");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+    f2* sw = reinterpret_cast<f2*>(smem_raw);  // two tiles [2][S / 2][P2]
+    const int P2 = k34_pitch(min(tx, nx), RW);
+    const int TB = (S / 2) * P2;  // float2 per tile buffer
+    const int t = threadIdx.x;
+    const int mb = cpg * NP * nbx;
+    const int kb = blockIdx.x >> 3;
+    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
+    if (g >= ngroups) return;
+    int m = kb % mb;
+    const int bx = m % nbx;
+    m /= nbx;
+    const int p = m % NP, ycl = m / NP;
+    const int nyg = (nyb + cpg - 1) / cpg;
+    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
+    if (yc >= nyb) return;
+    const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
+    const int xo0 = bx * tx;
+    const int txu = min(tx, nx - xo0);
+    const int sxs = max(xo0 - RW, 0);
+    const int ns = min(xo0 + txu + RW, nx) - sxs;
+    const int padL = sxs - (xo0 - RW), padR = (xo0 + txu + RW) - (sxs + ns);
+    const int npair = (ns + 1) >> 1;  // column pairs staged
+    const int wa = (npair + 63) >> 6;
+    const bool prod = t < NPT;
+    // producer waves with no staged column pair: every wave still takes one barrier per tile
+    // (a wave-uniform test, so the whole wave takes this branch)
+    if (prod && __builtin_amdgcn_readfirstlane(t >> 6) >= wa) {
+        for (int tt = 0; tt < (nrows + S - 1) / S; ++tt) {
+            lds_barrier();
+#ifdef OF3D_K34PK_SYNC2
+            lds_barrier();
+#endif
+        }
+        return;
+    }
+    f2 h[RW + 1];
+#pragma unroll
+    for (int k = 0; k <= RW; ++k) h[k] = (f2){hw[k], hw[k]};
+    const size_t pl = (size_t)zl * ny * nx;
+    const unsigned rowb = (unsigned)nx * 4u;
+    const int ntiles = (nrows + S - 1) / S;
+    if (prod) {
+        const unsigned vo0 = (unsigned)clampi(sxs + 2 * t, 0, nx - 1) * 4u;
+        const unsigned vo1 = (unsigned)clampi(sxs + 2 * t + 1, 0, nx - 1) * 4u;
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+        const bool lpad = padL > 0 && wv == 0;
+        const bool rpad = padR > 0 && wv == ((npair - 1) >> 6);
+        const int wpos = padL + 2 * t;  // tile column of this thread's first staged column
+        auto replicas = [&](f2* tile) {
+            if (lpad) {
+#pragma unroll
+                for (int q = 0; q < S / 2; ++q) {
+                    f2* row = tile + q * P2;
+                    const f2 e = row[padL];
+                    if (ln < padL) row[ln] = e;
+                }
+            }
+            if (rpad) {
+#pragma unroll
+                for (int q = 0; q < S / 2; ++q) {
+                    f2* row = tile + q * P2;
+                    const f2 e = row[padL + ns - 1];
+                    if (ln < padR) row[padL + ns + ln] = e;
+                }
+            }
+        };
+        constexpr unsigned long long pa = NP == 9 ? 0x311222312ull : 0x12212ull;
+        constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
+        const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
+        const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
+        auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
+        auto ld2 = [&](const __amdgpu_buffer_rsrc_t& r, unsigned o) {
+            return (f2){buf_ld<float>(r, vo0, o), buf_ld<float>(r, vo1, o)};
+        };
+        f2 ring[NR], ra[PD], rb[PD];
+#pragma unroll
+        for (int i = 0; i <= 2 * RW; ++i) {
+            const unsigned o = rowoff(i);
+            ring[i] = ld2(ra_, o) * ld2(rb_, o);
+        }
+#pragma unroll
+        for (int i = 0; i < PD; ++i) {
+            const unsigned o = rowoff(2 * RW + 1 + i);
+            ra[(2 * RW + 1 + i) % PD] = ld2(ra_, o);
+            rb[(2 * RW + 1 + i) % PD] = ld2(rb_, o);
+        }
+        for (int u0 = 0; u0 < nrows; u0 += NR) {
+            bool done = false;
+            [&]<int... H>(std::integer_sequence<int, H...>) {
+                (
+                    [&] {
+                        if (done) return;
+                        constexpr int h0 = H * S;
+                        f2* tile = sw + (((u0 + h0) / S) & 1) * TB;
+                        [&]<int... J>(std::integer_sequence<int, J...>) {
+                            (
+                                [&] {
+                                    constexpr int j = h0 + 2 * J;
+                                    constexpr int ic = j + 2 * RW + 1, ic1 = ic + 1;
+                                    ring[ic % NR] = ra[ic % PD] * rb[ic % PD];
+                                    const unsigned o = rowoff(u0 + ic + PD);
+                                    ra[ic % PD] = ld2(ra_, o);
+                                    rb[ic % PD] = ld2(rb_, o);
+                                    f2 p1 = ra[ic1 % PD] * rb[ic1 % PD];
+                                    const unsigned o1 = rowoff(u0 + ic1 + PD);
+                                    ra[ic1 % PD] = ld2(ra_, o1);
+                                    rb[ic1 % PD] = ld2(rb_, o1);
+                                    f2 a0 = ring[(j + RW) % NR] * h[0];
+                                    f2 a1 = ring[(j + 1 + RW) % NR] * h[0];
+                                    a0 = a0 + (ring[j % NR] + ring[(j + 2 * RW) % NR]) * h[RW];
+                                    a1 = a1 + (ring[(j + 1) % NR] + ring[(j + 1 + 2 * RW) % NR]) * h[RW];
+                                    ring[ic1 % NR] = p1;
+#pragma unroll
+                                    for (int k = RW - 1; k >= 1; --k) {
+                                        a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
+                                        a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
+                                    }
+                                    // rows j, j + 1 (pair (j % S) / 2) at columns wpos, wpos + 1
+                                    // (threads past the staged pairs write nothing: wpos would
+                                    // run into the next pair row)
+                                    if (t < npair) {
+                                        f2* q = tile + ((j % S) / 2) * P2 + wpos;
+                                        q[0] = (f2){a0.x, a1.x};
+                                        q[1] = (f2){a0.y, a1.y};
+                                    }
+                                }(),
+                                ...);
+                        }(std::make_integer_sequence<int, S / 2>{});
+                        replicas(tile);
+                        lds_barrier();  // tile published; the consumers are done with the other buffer
+#ifdef OF3D_K34PK_SYNC2
+                        lds_barrier();
+#endif
+                        if (u0 + h0 + S >= nrows) done = true;
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, NR / S>{});
+            if (done) break;
+        }
+    } else {
+        const int tb = t - NPT;
+        const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+        const int nseg = (txu + RB - 1) / RB;
+        constexpr int PP = S / 2, SPW = 64 / PP;  // pairs per tile; segments per wave item
+        const int nsgw = (nseg + SPW - 1) / SPW;
+        for (int tt = 0; tt < ntiles; ++tt) {
+            lds_barrier();  // tile tt written
+            const f2* tile = sw + (tt & 1) * TB;
+            const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
+            for (int i = tb; i < 64 * nsgw; i += NPT) {
+                const int l = i & 63, wg = i >> 6;
+                const int pr = l % PP, sg = wg * SPW + l / PP;
+                if (sg >= nseg) continue;
+                f2 out[RB];
+                lds_pass_c<RB, RW, DB>(tile + pr * P2, 1, RW + RB * sg, h, out);
+                const int c0 = RB * sg;
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2) {
+                    const int r = 2 * pr + e2;
+                    if (r < nr) {
+                        float o[RB];
+#pragma unroll
+                        for (int e = 0; e < RB; ++e) o[e] = e2 ? out[e].y : out[e].x;
+                        const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * 4u;
+                        if (c0 + RB <= txu) {
+                            buf_st_n<float, RB>(o, rq_, vo, 0);
+                        } else {
+                            for (int e = 0; e < RB; ++e)
+                                if (c0 + e < txu) buf_st<float>(o[e], rq_, vo + e * 4u, 0);
+                        }
+                    }
+                }
+            }
+#ifdef OF3D_K34PK_SYNC2
+            lds_barrier();
+#endif
         }
     }
 }

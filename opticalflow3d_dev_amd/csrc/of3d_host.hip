@@ -45,11 +45,12 @@ enum : unsigned {
     KU_K0C = 1u << 0, KU_K0 = 1u << 1, KU_K1C = 1u << 2, KU_K1 = 1u << 3, KU_K12 = 1u << 4, KU_K2C = 1u << 5,
     KU_K2 = 1u << 6, KU_K34 = 1u << 7, KU_K34WS = 1u << 8, KU_K3 = 1u << 9, KU_K4 = 1u << 10, KU_K5C = 1u << 11,
     KU_K5C_PK = 1u << 12, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
+    KU_K34PK = 1u << 17,
 };
 constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy_c",    "k_grad_xy",  "k_grad_xyz_c",
                                         "k_grad_z_c", "k_grad_z",     "k_prod_wyx",     "k_prod_wyx_ws", "k_prod_wy",
                                         "k_wx",       "k_wz_solve_c", "k_wz_solve_c2",  "k_wz_solve_dma", "k_wz_solve",
-                                        "k_solve2d",  "general"};
+                                        "k_solve2d",  "general",      "k_prod_wyx_pk"};
 
 struct of3d_plan {
     int ndim = 3;
@@ -86,7 +87,7 @@ struct of3d_plan {
         const void* fn = nullptr;
         int cw = 0, s = 0, tx = 0, nbx = 0;
         size_t lds = 0;
-        int nthr = 0;  // threads per block when not cw (wave-specialised: 2 cw)
+        int nthr = 0;  // threads per block when not cw (wave-specialised: 2 cw; packed fp32: cw)
     } k34;
     std::vector<K34Geom> k34_cand;  // geometries that keep >= 8 waves per CU (k34_tune picks)
     bool host_ev = false;            // host entry: record into ev[]
@@ -284,14 +285,22 @@ int k34_setup(of3d_plan* p, int np) {
                     int wsw = 0;
                     if (fw && lds <= 160 * 1024 && !occupancy(fw, 2 * cw, lds, wsw) && wsw >= 2 * nw)
                         p->k34_cand.push_back({fw, cw, s, tx, nbx, lds, 2 * cw});
+                    // fp32: the packed form (column pairs / row pairs on float2, 8-wave blocks)
+                    if constexpr (sizeof(F) == 4) {
+                        const void* fp = nw == 8 ? (np == 9 ? k34_fn_pk<9>(rw, s) : k34_fn_pk<5>(rw, s)) : nullptr;
+                        const size_t lpk = (size_t)s * k34_pitch(std::min(tx, nx), rw) * 8;
+                        int pkw = 0;
+                        if (fp && lpk <= 160 * 1024 && !occupancy(fp, cw, lpk, pkw) && pkw >= nw)
+                            p->k34_cand.push_back({fp, cw, s, tx, nbx, lpk, cw});
+                    }
                 }
             }
         }
     }
-    if (env_uq && env_uq[0] == '2') {  // experiments: the wave-specialised candidates only
+    if (env_uq && (env_uq[0] == '2' || env_uq[0] == '3')) {  // tests: wave-specialised (3: packed fp32) only
         std::vector<of3d_plan::K34Geom> ws;
         for (const auto& k : p->k34_cand)
-            if (k.nthr) ws.push_back(k);
+            if (k.nthr && (env_uq[0] == '2' || k.nthr == k.cw)) ws.push_back(k);
         p->k34_cand = ws;
         p->k34 = ws.empty() ? of3d_plan::K34Geom{} : ws.front();
     }
@@ -821,7 +830,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         const int ng = (int)(q1 - q0);
         const size_t o = (size_t)(q0 - R.zg0) * plane;
         OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st, (int)p->ya, (int)p->yb));
-        p->used |= p->k34.nthr ? KU_K34WS : KU_K34;
+        p->used |= p->k34.nthr ? (p->k34.nthr == p->k34.cw ? KU_K34PK : KU_K34WS) : KU_K34;
         return 0;
     };
     auto k3k4 = [&](hipStream_t st) -> int {  // fallback: W y and W x as two kernels (whole range)

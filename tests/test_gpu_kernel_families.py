@@ -14,7 +14,7 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK", "OF3D_K5C_NW")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK", "OF3D_K5C_NW", "OF3D_K34_UQ")
 
 
 def _run(img, s, t, w, ndim, mode, old, force=None, kernels=None):
@@ -151,5 +151,35 @@ def test_fused_w_kernels_wsig3_wsig6(case, fp32):
     old_used = []
     ref = _run(img, s, t, w, ndim, mode, old=True, kernels=old_used)
     assert not any(k.startswith("k_prod_wyx") for k in old_used), old_used
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_packed_fp32_products_w(case):
+    """The packed-fp32 K34 (k_prod_wyx_pk: float2 column pairs in W y, row pairs in W x,
+    v_pk_mul/add_f32) forced (OF3D_K34_UQ=3) against the older fp32 kernels: bit-identical."""
+    shape, (s, t, w), ndim = CASES[case]
+    img = np.random.default_rng(800 + case).integers(0, 4096, size=shape).astype(np.uint16)
+    if ndim == 2:
+        img = img[:, 0]
+    used = []
+    new = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=False, force={"OF3D_K34_UQ": "3"}, kernels=used)
+    assert "k_prod_wyx_pk" in used, used
+    ref = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", range(len(W_RADII)))
+def test_packed_fp32_products_w_radii(case):
+    shape, (s, t, w), ndim = W_RADII[case]
+    img = np.random.default_rng(900 + case).integers(0, 4096, size=shape).astype(np.uint16)
+    if ndim == 2:
+        img = img[:, 0]
+    used = []
+    new = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=False, force={"OF3D_K34_UQ": "3"}, kernels=used)
+    assert "k_prod_wyx_pk" in used, used
+    ref = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
