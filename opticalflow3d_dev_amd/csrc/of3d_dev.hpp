@@ -930,6 +930,11 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // arithmetic instead of alternating in lockstep.  One barrier per tile, two tile buffers:
 // producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
 // k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
+// Ablation at c3 (OF3D_EXP_K34_NOST / OF3D_EXP_K34_L2, timing only): without the W-xy
+// stores 1.13 ms (the VALU ideal at the measured clock) vs 1.72; gradient loads from one
+// cache-resident row 1.48.  Staging the stores through a wave-private LDS transpose (whole
+// rows per store instruction) measured slower (1.88 ms): the 72 B/voxel W-xy hand-off to
+// K5c itself, not its access pattern, is the cost.
 // (12-wave blocks — 4 consumer waves, 168 VGPRs, deeper prefetch, 8-row tiles — measured
 // slower: c3 1.95 vs 1.72 ms, c2 0.27 vs 0.19: the 16-wave occupancy hides more.)
 #ifndef OF3D_K34WS_PD
@@ -1010,7 +1015,11 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
         constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
         const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
         const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
+#ifndef OF3D_EXP_K34_L2
         auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
+#else  // experiment (timing only): every gradient load from one row (cache-resident)
+        auto rowoff = [&](int idx) { return (unsigned)clampi(y0 + (idx & 1), 0, ny - 1) * rowb; };
+#endif
         F ring[NR], ra[PD], rb[PD];
 #pragma unroll
         for (int i = 0; i <= 2 * RW; ++i) {
@@ -1085,7 +1094,11 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                 if (sg >= nseg) continue;
                 F out[RB];
                 lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
+#ifndef OF3D_EXP_K34_NOST
                 if (r < nr) {
+#else  // experiment (timing only): no W-xy stores
+                if (r < nr && out[0] == (F)1.2345e-30) {
+#endif
                     const int c0 = RB * sg;
                     const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
                     if (c0 + RB <= txu) {
