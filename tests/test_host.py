@@ -46,6 +46,58 @@ def test_tiff_roundtrip(tmp_path, dtype, shape):
     assert np.array_equal(np.asarray(m), a)
 
 
+def _raw_ifds(path):
+    """Every IFD of a little-endian classic TIFF as {tag: (type, count, values)} — a parser of
+    its own (TIFF 6.0 §2), independent of tiff.TiffFile."""
+    import struct
+    b = open(path, "rb").read()
+    assert b[:4] == b"II*\0"
+    size = {1: 1, 2: 1, 3: 2, 4: 4, 5: 8, 16: 8}
+    fmt = {1: "B", 2: "c", 3: "H", 4: "I", 16: "Q"}
+    out, off = [], struct.unpack_from("<I", b, 4)[0]
+    while off:
+        n = struct.unpack_from("<H", b, off)[0]
+        tags = {}
+        for i in range(n):
+            code, typ, cnt = struct.unpack_from("<HHI", b, off + 2 + 12 * i)
+            nb = size[typ] * cnt
+            at = off + 2 + 12 * i + 8 if nb <= 4 else struct.unpack_from("<I", b, off + 2 + 12 * i + 8)[0]
+            raw = b[at:at + nb]
+            tags[code] = (typ, cnt, raw if typ == 2 else struct.unpack("<%d%s" % (cnt, fmt[typ]), raw))
+        out.append(tags)
+        off = struct.unpack_from("<I", b, off + 2 + 12 * n)[0]
+    return b, out
+
+
+@pytest.mark.parametrize("dtype,bits,fmt", [(np.float32, 32, 3), (np.float64, 64, 3), (np.uint16, 16, 1)])
+def test_tiff_layout_pinned_by_spec(tmp_path, dtype, bits, fmt):
+    """The output files' tag set, pinned by specification (byte identity against tifffile
+    2025.3.13 is unverifiable here: tifffile is absent).  tifffile.imwrite(path, arr,
+    photometric='minisblack') of a (Z, Y, X) array — calc_flow.py:526-529 — writes one
+    uncompressed single-strip page per plane, tags in ascending order, the shaped-series JSON
+    description '{"shape": [Z, Y, X]}' on page 0 only, SampleFormat 3 for floats, data in
+    page order (contiguous, so readers memory-map it)."""
+    import json
+    a = np.random.default_rng(2).uniform(0, 9, size=(3, 5, 7)).astype(dtype)
+    p = tmp_path / "vx.tiff"
+    tf.imwrite(p, a, photometric="minisblack")
+    raw, ifds = _raw_ifds(p)
+    assert len(ifds) == 3
+    want = {254, 256, 257, 258, 259, 262, 273, 277, 278, 279, 305, 339}
+    plane = 5 * 7 * a.itemsize
+    for i, t in enumerate(ifds):
+        assert set(t) == want | ({270} if i == 0 else set())
+        assert t[254][2] == (0,) and t[256][2] == (7,) and t[257][2] == (5,)
+        assert t[258][2] == (bits,) and t[259][2] == (1,) and t[262][2] == (1,)  # none, minisblack
+        assert t[277][2] == (1,) and t[278][2] == (5,) and t[279][2] == (plane,) and t[339][2] == (fmt,)
+        assert t[273][2][0] == ifds[0][273][2][0] + i * plane  # contiguous, page order
+        assert t[273][2][0] % 2 == 0
+    desc = ifds[0][270][2].rstrip(b"\0").decode()
+    assert json.loads(desc) == {"shape": [3, 5, 7]} and desc == json.dumps({"shape": [3, 5, 7]})
+    o = ifds[0][273][2][0]
+    assert np.array_equal(np.frombuffer(raw[o:o + 3 * plane], dtype=dtype).reshape(a.shape), a)
+
+
 def test_tiff_bigtiff_roundtrip(tmp_path):
     a = np.arange(2 * 3 * 4, dtype=np.float64).reshape(2, 3, 4)
     p = tmp_path / "big.tiff"
