@@ -694,13 +694,19 @@ __device__ __forceinline__ F buf_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, uns
     else
         return __builtin_bit_cast(F, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
+// Cache policy of the buffer stores: OF3D_ST_NT=1 marks them non-temporal (gfx950 "nt":
+// streamed past L2 residency; every stored field is re-read only by a later kernel)
+#ifndef OF3D_ST_NT
+#define OF3D_ST_NT 0
+#endif
+constexpr int kStAux = OF3D_ST_NT ? 2 : 0;
 template <typename F>
 __device__ __forceinline__ void buf_st(F v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
     if constexpr (sizeof(F) == 8)
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0)), v),
-                                              r, voff, soff, 0);
+                                              r, voff, soff, kStAux);
     else
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, voff, soff, kStAux);
 }
 // N consecutive values from registers, as 16-byte stores (N * sizeof(F) a multiple of 16)
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -718,7 +724,7 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
 #pragma unroll
         for (int e = 0; e < PER; ++e) w[e] = v[i + e];
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, w), r, voff + i * (unsigned)sizeof(F), soff,
-                                               0);
+                                               kStAux);
     }
 }
 
@@ -1123,6 +1129,9 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
 // producer's two rows j, j + 1 of columns c, c + 1 are the pair row j / 2 at x = c, c + 1.
 // Pair pitch P2 = 1 (mod 32) float2: the consumers' 4 pairs x 4 segments of a 16-lane
 // group hit 32 distinct banks.  Ring, prefetch and tile double-buffering as k_prod_wyx_ws.
+#ifndef OF3D_K34PK_LD64
+#define OF3D_K34PK_LD64 1
+#endif
 template <int NP, int RW, int S, int PD = 2, int DB = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_prod_wyx_pk(const float* __restrict__ G, float* __restrict__ Q, int ny,
                                                      int nx, size_t fs, const float* __restrict__ hw, int tx,
@@ -1204,9 +1213,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
         const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
         auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
+#if OF3D_K34PK_LD64
+        // the column pair as ONE 8-byte load (dword-aligned buffer load): columns c, c + 1 when
+        // both are inside the row, else the row's last two with the last one duplicated (the
+        // clamped pair of the scalar form)
+        const int cp = sxs + 2 * t;
+        const bool dup = cp > nx - 2;
+        const unsigned vp = (unsigned)(dup ? nx - 2 : cp) * 4u;
+        (void)vo0, (void)vo1;
+        auto ld2 = [&](const __amdgpu_buffer_rsrc_t& r, unsigned o) {
+            f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, vp, o, 0));
+            if (dup) v.x = v.y;
+            return v;
+        };
+#else
         auto ld2 = [&](const __amdgpu_buffer_rsrc_t& r, unsigned o) {
             return (f2){buf_ld<float>(r, vo0, o), buf_ld<float>(r, vo1, o)};
         };
+#endif
         f2 ring[NR], ra[PD], rb[PD];
 #pragma unroll
         for (int i = 0; i <= 2 * RW; ++i) {
