@@ -695,7 +695,8 @@ __device__ __forceinline__ F buf_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, uns
         return __builtin_bit_cast(F, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 // Cache policy of the buffer stores: OF3D_ST_NT=1 marks them non-temporal (gfx950 "nt":
-// streamed past L2 residency; every stored field is re-read only by a later kernel)
+// streamed past L2 residency; every stored field is re-read only by a later kernel).  Measured
+// neutral (c3 fp64 3.707 vs 3.718 ms, c3 fp32 2.071 vs 2.110, c5 fp32 120.65 vs 120.76): off.
 #ifndef OF3D_ST_NT
 #define OF3D_ST_NT 0
 #endif

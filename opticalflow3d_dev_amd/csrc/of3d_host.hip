@@ -324,7 +324,10 @@ int k5c_setup(of3d_plan* p) {
     if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
     if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
     const char* er = getenv("OF3D_K5C_R");
-    const int r = er ? atoi(er) : 8;
+    // planes per z-group: 8 (64-plane blocks) or 4 (32).  A 128-plane fp32 instance (R 16, 4 waves,
+    // 191 VGPRs, two blocks per CU) measured slower: c5 fp32 41.8 vs 39.7 ms, c3 fp32 0.74 vs 0.68
+    int r = er ? atoi(er) : 8;
+    if (r != 4) r = 8;  // the instances compiled (k5c_fn): the launch grid must match them
     // fp32: the packed kernel (two columns per lane as float2; window bytes as the fp64 kernel's)
     const void* pk = nullptr;
     if constexpr (sizeof(F) == 4) {
