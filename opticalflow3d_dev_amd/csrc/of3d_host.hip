@@ -785,12 +785,13 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             const int tx = p->rd == 3 ? k12_tx<3>() : (p->rd == 6 ? k12_tx<6>() : k12_tx<9>());
             int nbx = (int)cdiv(nx, tx), ntile = nbx * (int)cdiv(ny, K12_TY);
             int zin0 = (int)R.zb0, nzc = (int)R.zb1, zg0 = (int)R.zg0, qa = (int)q0, nq = ng;
-            // planes per block: the longest march that still gives >= 1024 blocks (each march
-            // re-forms 2 rd halo planes), at least 16
+            // planes per block: the longest march (up to 256) that still gives >= 1024 blocks
+            // (each march re-forms 2 rd halo planes), at least 16.  Measured: c5 fp32 K12 20.7 /
+            // 20.0 / 19.7 ms at 64 / 128 / 256, c4 fp64 4.40 / 4.12 at 64 / 128; c3 keeps 64
             static const int zc_env = getenv("OF3D_K12_ZC") ? atoi(getenv("OF3D_K12_ZC")) : 0;
             int zc = zc_env;
             if (zc <= 0) {
-                zc = 64;
+                zc = 256;
                 while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;
             }
             const unsigned gx = 8 * cdiv(ntile, 8);
