@@ -377,7 +377,11 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     if (yb1 < 0) yb1 = ny;
     const int nyo = yb1 - yb0;  // output rows (row-slab plans: the own rows)
     const int nyb_max = std::max(1, nyo / 32);
-    static const long target = 4L * 256 * 2 * (getenv("OF3D_K34_NYBX") ? atol(getenv("OF3D_K34_NYBX")) : 2);
+    // block target: 4096 for the lockstep / packed kernels; 2048 for the 16-wave wave-specialised
+    // one (one block per CU: longer row chunks re-read fewer halo rows — c3 K34 1.65 vs 1.71 ms
+    // at 4096, 1.85 at 8192; c4 neutral).  OF3D_K34_NYBX scales it (experiments).
+    static const double tscale = getenv("OF3D_K34_NYBX") ? atof(getenv("OF3D_K34_NYBX")) : 1.0;
+    const long target = std::max(1L, (long)((k.nthr == 1024 ? 2048.0 : 4096.0) * tscale));
     int nyb = 1;
     while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
     int nyc = (nyo + nyb - 1) / nyb;
