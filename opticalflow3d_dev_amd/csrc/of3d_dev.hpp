@@ -2059,6 +2059,35 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
+// K5c block coordinates from the launch's (columns, rows, z chunks) grid, XCD-aware: the
+// linear workgroup id b runs on XCD b % 8, so the z chunks of one (column block, row) — whose
+// windows share 2 rw W-xy planes — get ids 8 apart (same XCD, dispatched back to back) and
+// the shared planes come from that XCD's L2 instead of HBM twice.  A bijection on the grid
+// (the tail past the last whole group of 8 z-chunk sets keeps the plain order).
+#ifndef OF3D_K5C_XCD
+#define OF3D_K5C_XCD 1
+#endif
+struct K5Block {
+    int bx, by, bz;
+};
+__device__ __forceinline__ K5Block k5c_block() {
+    if (!OF3D_K5C_XCD || gridDim.z == 1) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const unsigned gx = gridDim.x, gxy = gx * gridDim.y, nz = gridDim.z;
+    const unsigned b = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned full = (gxy * nz) / (8 * nz) * (8 * nz);
+    unsigned rest, zc;
+    if (b < full) {
+        const unsigned j = b >> 3;
+        zc = j % nz;
+        rest = (j / nz) * 8 + (b & 7);
+    } else {
+        const unsigned l = b - full;
+        zc = l % nz;
+        rest = full / nz + l / nz;
+    }
+    return {(int)(rest % gx), (int)(rest / gx), (int)zc};
+}
+
 // K5c: the LDS-DMA W z + solve with a compile-time window radius (taps in SGPRs,
 // lds_pass_c: no weight loads or waits inside the passes) and narrow blocks: CB = 32
 // columns x 2 z-groups per wave, 4 waves (256 threads), R planes per z-group, so a
@@ -2082,11 +2111,12 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
     F* sm = reinterpret_cast<F*>(smem_raw);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int col = lane % CB, gz = w * LPC + lane / CB;
-    const int x = blockIdx.x * CB + col;
-    const int y = yo0 + blockIdx.y;  // outputs: rows [yo0, yo0 + gridDim.y) in a compact layout
-    const int zc0 = zo0 + blockIdx.z * ZC;
+    const K5Block kb = k5c_block();
+    const int x = kb.bx * CB + col;
+    const int y = yo0 + kb.by;  // outputs: rows [yo0, yo0 + gridDim.y) in a compact layout
+    const int zc0 = zo0 + kb.bz * ZC;
     const size_t ps = (size_t)ny * nx;
-    const int xc = min((int)blockIdx.x * CB + EPL * (lane % LPR), nx - EPL);  // this lane's DMA columns
+    const int xc = min(kb.bx * CB + EPL * (lane % LPR), nx - EPL);  // this lane's DMA columns
     const F* qrow = Q + (size_t)y * nx + xc;
     const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
     F h[RW + 1];
@@ -2130,7 +2160,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
     }
     if (x >= nx) return;
 #ifndef OF3D_EXP_K5_NOSOLVE
-    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)blockIdx.y * nx + x, (size_t)gridDim.y * nx, vx,
+    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
                                vy, vz, rel);
 #else  // experiment: no solve / eigenvalue (stores the field sums)
 #pragma unroll
@@ -2139,7 +2169,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         F a = acc[0][i];
 #pragma unroll
         for (int f = 1; f < 9; ++f) a = a + acc[f][i];
-        const size_t o = (size_t)(zc0 + gz * R - zo0 + i) * gridDim.y * nx + (size_t)blockIdx.y * nx + x;
+        const size_t o = (size_t)(zc0 + gz * R - zo0 + i) * gridDim.y * nx + (size_t)kb.by * nx + x;
         vx[o] = a;
         vy[o] = a;
         vz[o] = a;
