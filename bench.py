@@ -132,7 +132,8 @@ def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane, sv=8):
     }
 
 
-STAGE_KERNELS = {"grad_xy": ("k_tderiv", "k_grad_xy"), "grad_z": ("k_grad_z",), "prod_wy": ("k_prod_wy",),
+STAGE_KERNELS = {"grad_xy": ("k_tderiv", "k_grad_xy_", "k_grad_xy<"), "grad_z": ("k_grad_z", "k_grad_xyz"),
+                 "prod_wy": ("k_prod_wy",),
                  "prod_wy_wx": ("k_prod_wyx",), "wx": ("k_wx",), "wz_solve": ("k_wz_solve",)}
 
 
@@ -145,9 +146,17 @@ def fused_names(profile):
     return profile
 
 
-def load_pmc_traffic(stage, cfg):
+# kernel families a plan reports (of3d_plan_kernels; kKernelNames in csrc/of3d_host.hip)
+PLAN_FAMILIES = {"k_tderiv_c", "k_tderiv", "k_grad_xy_c", "k_grad_xy", "k_grad_xyz_c", "k_grad_z_c", "k_grad_z",
+                 "k_prod_wyx", "k_prod_wyx_ws", "k_prod_wy", "k_wx", "k_wz_solve_c", "k_wz_solve_c2",
+                 "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk"}
+
+
+def load_pmc_traffic(stage, cfg, used=None):
     """HBM bytes per launch of the stage's kernels from the committed rocprofv3 PMC summary
-    (profiles/pmc_<cfg>.json: FETCH_SIZE x2 + WRITE_SIZE, calibrated in profiles/pmc_calibration.json)."""
+    (profiles/pmc_<cfg>.json: FETCH_SIZE x2 + WRITE_SIZE, calibrated in profiles/pmc_calibration.json).
+    used: the families the measured plan launched (plan.kernels()); a known family it did not
+    launch (a K34 autotune candidate of another family) is not counted."""
     path = os.path.join(REPO, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
         return None
@@ -162,6 +171,8 @@ def load_pmc_traffic(stage, cfg):
             for pre in STAGE_KERNELS[stage]:
                 if k.startswith(pre):
                     base = k.split("<")[0]
+                    if used and base in PLAN_FAMILIES and base not in used:
+                        continue
                     rank = (e.get("dispatches", 0), -e.get("profiled_ms", 0.0))
                     if base not in best or rank > best[base][0]:
                         best[base] = (rank, e)
@@ -289,7 +300,7 @@ def frame_ops_per_voxel(rd, rs, rt, rw):
     return C(rt) + 3 * C(rd) + 3 * (C(rd) + 2 * C(rs)) + 9 + 27 * C(rw) + 65 + 50
 
 
-def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=8):
+def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=8, used=None):
     """roofline object of the bench line.
 
     The exact fp64 path is VALU-bound by construction (28-37 algorithmic
@@ -309,7 +320,7 @@ def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=
     return {
         "bound": "valu", "kernel": dom, "achieved": round(ach, 3), "peak": peak_v,
         "unit": "Top/s (%s add/mul lane-ops, no FMA)" % ("fp64" if sv == 8 else "fp32"),
-        "frac": round(ach / peak_v, 4), "traffic": load_pmc_traffic(dom, cfg),
+        "frac": round(ach / peak_v, 4), "traffic": load_pmc_traffic(dom, cfg, used),
         "algorithmic_ops_per_launch": model[dom]["ops"], "avg_launch_ms": round(dom_ms, 5),
         "kernel_hbm": {"workspace_bytes_per_launch": model[dom]["bytes"], "achieved_GBs": round(k_gbs, 2),
                        "frac": round(k_gbs / HBM_PEAK_GBS, 4)},
@@ -430,7 +441,8 @@ def run_slab(args, world, rank, local_rank, dev):
             nb = no = ng = nz
             plane = (ai1 - ai0) * nx
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, plane, sv), args.config,
-                        (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv)
+                        (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv,
+                        used=set(plan.kernels()))
         roof["frame"]["note"] = "this rank's share: %s %d..%d (with halo %d..%d) of %d" % (
             "planes" if axis == 0 else "rows", a0, a1, ai0, ai1, n_ax)
         cpu = None
@@ -538,7 +550,7 @@ def main():
         value = world * vox * args.steps / elapsed / 1e6
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
                         args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox,
-                        frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv)
+                        frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv, used=set(plan.kernels()))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             sub = min(cpu_sample_planes(nz, ny, nx, args.cpu_budget), nz)
