@@ -368,8 +368,7 @@ int k5c_setup(of3d_plan* p) {
 }
 
 // One K34 launch over ng planes of nf products.  Rows are cut into chunks of >= 32
-// rows (each chunk re-reads 2 rw halo rows) until there are >= 4096 blocks (measured
-// 2-3 % faster than 2048 on c2/c3: shorter tail); blocks of one group share an XCD: all row chunks of a plane when there are
+// rows (each chunk re-reads 2 rw halo rows) until there are >= 2048 blocks; blocks of one group share an XCD: all row chunks of a plane when there are
 // planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
 template <typename K, typename F>
 hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
@@ -377,11 +376,11 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     if (yb1 < 0) yb1 = ny;
     const int nyo = yb1 - yb0;  // output rows (row-slab plans: the own rows)
     const int nyb_max = std::max(1, nyo / 32);
-    // block target: 4096 for the lockstep / packed kernels; 2048 for the 16-wave wave-specialised
-    // one (one block per CU: longer row chunks re-read fewer halo rows — c3 K34 1.65 vs 1.71 ms
-    // at 4096, 1.85 at 8192; c4 neutral).  OF3D_K34_NYBX scales it (experiments).
+    // block target 2048: longer row chunks re-read fewer halo rows (c3 wave-specialised K34 1.67
+    // vs 1.76 ms at 4096, 1.73 at 1024; c2 lockstep K34 0.175 vs 0.191 ms, frame 0.420 vs 0.435;
+    // c4 neutral).  OF3D_K34_NYBX scales it (experiments).
     static const double tscale = getenv("OF3D_K34_NYBX") ? atof(getenv("OF3D_K34_NYBX")) : 1.0;
-    const long target = std::max(1L, (long)((k.nthr == 1024 ? 2048.0 : 4096.0) * tscale));
+    const long target = std::max(1L, (long)(2048.0 * tscale));
     int nyb = 1;
     while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
     int nyc = (nyo + nyb - 1) / nyb;
