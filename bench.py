@@ -14,7 +14,13 @@ selects configs[1]; c4/c5 are the z-slab (strong-scaling) configs.
 N > 1 (torch.distributed.run, one rank per GPU): frame replicas — every rank
 computes its own output frame (calc_flow.py:512 marks output frames as the
 independent axis); no data-path collective; value = all ranks' voxels / max
-rank time.  Rank 0 prints ONE JSON line.
+rank time.  Beside it, the line's "strong" object: the same frame split over
+the ranks as z-slabs (and row slabs where they carry less halo work), each
+step the newest frame's rd + rw halo exchanged over RCCL P2P beside the
+previous step's compute — per-rank compute, exchange and pipelined step times
+and the efficiency against the one-GPU frame.  Rank 0 prints ONE JSON line,
+with "parity_sample": one output crop checked against the oracle outside the
+timed region, and "build": the library's source hash (of3d_build_info).
 
 Roofline: the dominant kernel's average duration from HIP events recorded on
 the launch stream over the timed region (of3d_plan_set_timing ring), with its
@@ -333,19 +339,173 @@ def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=
     }
 
 
-def run_slab(args, world, rank, local_rank, dev):
-    """configs[3] / configs[4]: ONE volume per output frame, split over the ranks (strong
-    scaling), as process_flow runs a time series of it: each rank holds its own part (z-planes
-    or rows: --split, default the axis with less halo work, shard.slab_axis) of 2*rt+2
-    resident frames; a step = the newest frame's halo exchange with the neighbours (RCCL
-    P2P, on its own stream, beside the previous step's compute) + the rank's compute.
-    OF3D_BENCH_VRANK="r/P": time rank r of a P-way split on this one GPU (no exchange) —
-    the per-rank compute the scaling model in DESIGN.md uses."""
+class SlabBench:
+    """One rank's share of ONE volume per output frame, split over the ranks (strong scaling),
+    as process_flow's slab path runs a time series of it (stream.FlowStream(zslab=...)): the
+    rank holds its own part (z-planes: axis 0, or rows: axis 1) plus the rd + rw halo of
+    2*rt+2 resident frames; a step = the newest frame's halo exchange with the neighbours
+    (shard.exchange_frame_halo: RCCL P2P on its own stream, beside the previous step's
+    compute) + the rank's compute.  vrank=(r, P): rank r of a P-way split on this one GPU,
+    no exchange (the per-rank compute of the scaling model)."""
+
+    def __init__(self, dims, sig, axis, rank, world, dev, fp32=False, timing=0, vrank=None, seed=20260206):
+        import torch
+
+        from opticalflow3d_dev_amd import _lib, make_taps, radii
+        from opticalflow3d_dev_amd.shard import check_slab_split, halo_planes, zslab_bounds
+
+        nz, ny, nx = dims
+        s, t, w = sig
+        self.dims, self.axis, self.rank, self.world, self.dev = dims, axis, rank, world, dev
+        self.rd, self.rs, self.rt, self.rw = radii(s, t, w)
+        self.nwin = 2 * self.rt + 1
+        self.fp32 = fp32
+        self.vrank = vrank
+        prank, pworld = vrank if vrank else (rank, world)
+        self.n_ax = nz if axis == 0 else ny
+        check_slab_split(self.n_ax, pworld)
+        self.a0, self.a1 = zslab_bounds(self.n_ax, prank, pworld)
+        self.ai0, self.ai1 = (halo_planes(self.n_ax, self.a0, self.a1, self.rd, self.rw) if pworld > 1
+                              else (0, self.n_ax))
+        mode = _lib.OF3D_FP32 if fp32 else 0
+        taps = make_taps(s, t, w)
+        self.rows_direct = False
+        if axis == 0:
+            self.plan = _lib.Plan(3, nz, ny, nx, taps, device=dev.index, max_out_planes=self.a1 - self.a0,
+                                  timing=timing, mode=mode)
+            self.blk_shape = (self.ai1 - self.ai0, ny, nx)
+        else:
+            self.plan = _lib.Plan(3, nz, self.ai1 - self.ai0, nx, taps, device=dev.index, timing=timing, mode=mode)
+            self.blk_shape = (nz, self.ai1 - self.ai0, nx)
+            self.rows_direct = os.environ.get("OF3D_BENCH_ROWS", "1") == "1"
+            if self.rows_direct:
+                try:  # the W kernels write only the own rows (halo rows only in K0 / gradients / W y)
+                    self.plan.set_rows(self.a0 - self.ai0, self.a1 - self.ai0)
+                except RuntimeError:
+                    self.rows_direct = False
+        # 2 rt + 2 slots: the step's exchange goes to the slot the frame before last read
+        self.ring = torch.empty((self.nwin + 1,) + self.blk_shape, dtype=torch.int16, device=dev)
+        for f in range(self.nwin + 1):
+            if axis == 0:
+                synthetic_slab(1, nz, ny, nx, self.ai0, self.ai1, seed + f, dev, out=self.ring[f:f + 1])
+            else:
+                synthetic_slab(1, nz, ny, nx, 0, nz, seed + f, dev, out=self.ring[f:f + 1], rows=(self.ai0, self.ai1))
+        self.own = (self.a1 - self.a0) * (ny * nx if axis == 0 else nz * nx)
+        n_out = self.own if (axis == 0 or self.rows_direct) else int(np.prod(self.blk_shape))
+        vt = torch.float32 if fp32 else torch.float64
+        self.n_out = n_out
+        self.outs = [torch.empty(max(n_out, 1), dtype=vt, device=dev) for _ in range(3)]
+        self.rel = torch.empty(max(n_out, 1), dtype=torch.float32, device=dev)
+        self.comp = torch.cuda.current_stream(dev)
+        self.xs = torch.cuda.Stream(device=dev)
+        self.done = {}  # slot -> event of the last compute that read it
+        self.order = list(range(self.nwin))
+
+    def _xchg_view(self, slot):
+        v = self.ring[slot]
+        return v if self.axis == 0 else v.transpose(0, 1)
+
+    def exchange(self, slot):
+        from opticalflow3d_dev_amd.shard import exchange_frame_halo
+
+        exchange_frame_halo(self._xchg_view(slot), self.ai0, self.a0, self.a1, self.n_ax, self.rd + self.rw,
+                            self.rank, self.world)
+
+    def step(self, exchange=True, compute=True):
+        """The newest frame into the free slot (its halo exchanged on the side stream), then the
+        rank's compute on the compute stream behind it."""
+        import torch
+
+        from opticalflow3d_dev_amd import _lib
+
+        new = (self.order[-1] + 1) % (self.nwin + 1)  # the free slot takes the newest frame
+        if exchange and self.world > 1 and not self.vrank:
+            with torch.cuda.stream(self.xs):
+                if new in self.done:
+                    self.xs.wait_event(self.done[new])
+                self.exchange(new)
+                ev = torch.cuda.Event()
+                ev.record(self.xs)
+            self.comp.wait_event(ev)
+        self.order.pop(0)
+        self.order.append(new)
+        if not compute:
+            return
+        ptrs = [self.ring[sl].data_ptr() for sl in self.order]
+        o = [t.data_ptr() for t in self.outs] + [self.rel.data_ptr()]
+        if self.axis == 0:
+            self.plan.execute(ptrs, _lib.OF3D_U16, self.ai0, self.a0, self.a1, *o, self.comp.cuda_stream)
+        else:
+            self.plan.execute(ptrs, _lib.OF3D_U16, 0, 0, self.dims[0], *o, self.comp.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(self.comp)
+        for sl in self.order:
+            self.done[sl] = ev
+
+    def finite(self):
+        return bool(self.outs[0][:self.n_out].isfinite().all().item()) if self.n_out else True
+
+    def describe(self):
+        split = "z-slabs" if self.axis == 0 else "row slabs"
+        return "%s: %s %d..%d (with halo %d..%d) of %d" % (split, "planes" if self.axis == 0 else "rows", self.a0,
+                                                           self.a1, self.ai0, self.ai1, self.n_ax)
+
+    def close(self):
+        import torch
+
+        torch.cuda.synchronize(self.dev)
+        self.plan.close()
+
+
+def timed_steps(step, steps, warmup, world, dev):
+    """warmup, then `steps` steps between barrier + synchronize; max over ranks (s)."""
     import torch
     import torch.distributed as dist
 
-    from opticalflow3d_dev_amd import _lib, make_taps, radii
-    from opticalflow3d_dev_amd.shard import exchange_frame_halo, halo_planes, slab_axis, zslab_bounds
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    return max_over_ranks([el], dev)[0] if world > 1 else el
+
+
+def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms):
+    """The default workload's frame split over the N ranks (strong scaling) — the path
+    configs[3]/[4] and process_flow(parallel="zslab"/"yslab") run, on the headline volume:
+    per-rank compute alone, the halo exchange alone (RCCL P2P of the newest frame's rd + rw
+    planes / rows), and the pipelined step (exchange beside the previous step's compute).
+    efficiency = the one-GPU frame time t1 (this run's replica step) / (N * step)."""
+    nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
+    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50)
+    try:
+        comp = timed_steps(lambda: sb.step(exchange=False), steps, warmup, world, dev)
+        xchg = timed_steps(lambda: sb.step(compute=False), steps, warmup, world, dev)
+        both = timed_steps(sb.step, steps, warmup, world, dev)
+        finite = sb.finite()
+        desc = sb.describe()
+    finally:
+        sb.close()
+    ms = both / steps * 1e3
+    return {"split": "z-slabs" if axis == 0 else "row slabs", "halo": sb.rd + sb.rw, "rank0_part": desc,
+            "ms_per_step": round(ms, 5), "value": round(nz * ny * nx / (ms * 1e-3) / 1e6, 3), "unit": "Mvoxels/s",
+            "compute_ms_max_rank": round(comp / steps * 1e3, 5), "exchange_ms": round(xchg / steps * 1e3, 5),
+            "efficiency_vs_one_gpu_frame": round(t1_ms / (world * ms), 4), "outputs_finite_rank0": finite}
+
+
+def run_slab(args, world, rank, local_rank, dev):
+    """configs[3] / configs[4]: ONE volume per output frame, split over the ranks (strong
+    scaling) — SlabBench.  OF3D_BENCH_VRANK="r/P": time rank r of a P-way split on this one
+    GPU (no exchange) — the per-rank compute the scaling model in DESIGN.md uses."""
+    from opticalflow3d_dev_amd import radii
+    from opticalflow3d_dev_amd.shard import slab_axis
 
     nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
     rd, rs, rt, rw = radii(s, t, w)
@@ -357,83 +517,19 @@ def run_slab(args, world, rank, local_rank, dev):
     axis = {"z": 0, "y": 1}.get(args.split, None)
     if axis is None:
         axis = slab_axis(nz, ny, pworld, rd, rw)
-    n_ax = nz if axis == 0 else ny
-    a0, a1 = zslab_bounds(n_ax, prank, pworld)
-    ai0, ai1 = halo_planes(n_ax, a0, a1, rd, rw) if pworld > 1 else (0, n_ax)
-    mode = _lib.OF3D_FP32 if fp32 else 0
-    taps = make_taps(s, t, w)
-    rows_direct = False
-    if axis == 0:
-        plan = _lib.Plan(3, nz, ny, nx, taps, device=dev.index, max_out_planes=max(a1 - a0, 1),
-                         timing=max(args.steps, 1), mode=mode)
-        blk_shape = (ai1 - ai0, ny, nx)
-    else:
-        plan = _lib.Plan(3, nz, ai1 - ai0, nx, taps, device=dev.index, timing=max(args.steps, 1), mode=mode)
-        blk_shape = (nz, ai1 - ai0, nx)
-        rows_direct = os.environ.get("OF3D_BENCH_ROWS", "1") == "1"
-        if rows_direct:
-            try:  # the W kernels write only the own rows (halo rows only in K0 / gradients / W y)
-                plan.set_rows(a0 - ai0, a1 - ai0)
-            except RuntimeError:
-                rows_direct = False
-    nblk = int(np.prod(blk_shape))
     seed = 20260206 + (5 if fp32 else 4)
-    # 2 rt + 2 slots: the step's exchange goes to the slot the frame before last read
-    ring = torch.empty((nwin + 1,) + blk_shape, dtype=torch.int16, device=dev)
-    for f in range(nwin + 1):
-        if axis == 0:
-            synthetic_slab(1, nz, ny, nx, ai0, ai1, seed + f, dev, out=ring[f:f + 1])
-        else:
-            synthetic_slab(1, nz, ny, nx, 0, nz, seed + f, dev, out=ring[f:f + 1], rows=(ai0, ai1))
-    n_full = (a1 - a0) * (ny * nx if axis == 0 else nz * nx) if (axis == 0 or rows_direct) else nblk
-    vt = torch.float32 if fp32 else torch.float64
-    outs = [torch.empty(max(n_full, 1), dtype=vt, device=dev) for _ in range(3)]
-    rel = torch.empty(max(n_full, 1), dtype=torch.float32, device=dev)
-    comp = torch.cuda.current_stream(dev)
-    xs = torch.cuda.Stream(device=dev)
-    done = {}  # slot -> event of the last compute that read it
-    order = list(range(nwin))
-    state = {"k": 0}
-
-    def xchg_view(slot):
-        v = ring[slot]
-        return v if axis == 0 else v.transpose(0, 1)
-
-    def step():
-        k = state["k"]
-        state["k"] += 1
-        new = (order[-1] + 1) % (nwin + 1)  # the free slot takes the newest frame
-        if world > 1 and not vr:
-            with torch.cuda.stream(xs):
-                if new in done:
-                    xs.wait_event(done[new])
-                exchange_frame_halo(xchg_view(new), ai0, a0, a1, n_ax, rd + rw, rank, world)
-                ev = torch.cuda.Event()
-                ev.record(xs)
-            comp.wait_event(ev)
-        order.pop(0)
-        order.append(new)
-        ptrs = [ring[sl].data_ptr() for sl in order]
-        if axis == 0:
-            plan.execute(ptrs, _lib.OF3D_U16, ai0, a0, a1, outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
-                         rel.data_ptr(), comp.cuda_stream)
-        else:
-            plan.execute(ptrs, _lib.OF3D_U16, 0, 0, nz, outs[0].data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
-                         rel.data_ptr(), comp.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(comp)
-        for sl in order:
-            done[sl] = ev
-        del k
-
-    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
-    finite = bool(torch.isfinite(outs[0][:n_full]).all().item()) if n_full else True
+    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32, timing=max(args.steps, 1),
+                   vrank=(prank, pworld) if vr else None, seed=seed)
+    plan = sb.plan
+    elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev)
+    finite = sb.finite()
     if world > 1:
         elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
         finite = bad == 0.0
     if rank == 0:
         vox = nz * ny * nx
-        own = (a1 - a0) * (ny * nx if axis == 0 else nz * nx)
+        own = sb.own
+        ai0, ai1, a0, a1 = sb.ai0, sb.ai1, sb.a0, sb.a1
         if axis == 0:
             nb, no, ng = ai1 - ai0, a1 - a0, min(a1 + rw, nz) - max(a0 - rw, 0)
             plane = ny * nx
@@ -443,8 +539,7 @@ def run_slab(args, world, rank, local_rank, dev):
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, plane, sv), args.config,
                         (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv,
                         used=set(plan.kernels()))
-        roof["frame"]["note"] = "this rank's share: %s %d..%d (with halo %d..%d) of %d" % (
-            "planes" if axis == 0 else "rows", a0, a1, ai0, ai1, n_ax)
+        roof["frame"]["note"] = "this rank's share: " + sb.describe()
         cpu = None
         if world == 1 and not vr and not args.no_cpu_baseline:
             sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
@@ -463,10 +558,50 @@ def run_slab(args, world, rank, local_rank, dev):
                                        f"{split} x{world}, halo {rd + rw}" if world > 1 else "single GPU (whole frame)"),
                        "inputs": "own part of 2*rt+2 uint16 frames resident in HBM; per step the newest frame's "
                                  "halo exchange (RCCL P2P, own stream) + compute", "outputs_finite": finite},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "build": build_stamp(),
         }
         print(json.dumps(line), flush=True)
-    plan.close()
+    sb.close()
+
+
+def build_stamp():
+    """The loaded library's provenance (of3d_build_info: source hash, flags; the tree's hash)."""
+    from opticalflow3d_dev_amd import _lib
+
+    i = _lib.build_info()
+    return {"src_hash": i["src_hash"], "tree_hash": i["tree_hash"], "extra": i["extra"], "lib": i["lib"]}
+
+
+def parity_sample(d_in, outs, box, s, t, w, fp32=False):
+    """The headline run's outputs checked against the oracle (oracle/cpu_ref.py, the CPU
+    restatement pinned to the reference) on one crop — outside the timed region, the checker
+    only.  Output voxels further than rd + rw from every face where the crop cuts the volume
+    are exact (tests/test_gpu_bench_geometry.py); vx/vy/vz must match bit for bit (fp32
+    runs: within 1e-4 max|v|), rel within 1e-6 lambda_max."""
+    from oracle import cpu_ref
+    from opticalflow3d_dev_amd import radii
+
+    rd, _, _, rw = radii(s, t, w)
+    h = rd + rw
+    nt, nz, ny, nx = d_in.shape
+    z0, z1, y0, y1, x0, x1 = box
+    lo = [max(a - h, 0) for a in (z0, y0, x0)]
+    hi = [min(b + h, n) for b, n in zip((z1, y1, x1), (nz, ny, nx))]
+    sub = np.ascontiguousarray(d_in[:, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]].cpu().numpy().view(np.uint16))
+    st = cpu_ref.structure_tensor3d(sub, s, t, w, backend="scipy")
+    want = cpu_ref.solve3d(st)
+    lmin, lmax = cpu_ref.eig_fp64_3d(st)
+    sl = (slice(z0 - lo[0], z1 - lo[0]), slice(y0 - lo[1], y1 - lo[1]), slice(x0 - lo[2], x1 - lo[2]))
+    got = [o.view(nz, ny, nx)[z0:z1, y0:y1, x0:x1].cpu().numpy() for o in outs]
+    if fp32:
+        dv = max(float(np.abs(g.astype(np.float64) - v[sl]).max() / np.abs(v[sl]).max()) for g, v in zip(got, want))
+        ok_v = dv <= 1e-4
+    else:
+        ok_v = all(np.array_equal(g.view(np.uint64), v[sl].view(np.uint64)) for g, v in zip(got, want))
+    rel_err = float(np.max(np.abs(got[3].astype(np.float64) - lmin[sl]) / (np.abs(lmax[sl]) + 1e-300)))
+    ok = bool(ok_v and rel_err <= (1e-4 if fp32 else 1e-6))
+    return {"ok": ok, "crop_out": list(box), "vxyz": ("within 1e-4 max|v|" if fp32 else "bitwise") if ok_v else
+            "MISMATCH", "rel_max_err_over_lmax": rel_err, "checker": "oracle/cpu_ref.py (scipy backend)"}
 
 
 def main():
@@ -482,6 +617,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
     ap.add_argument("--split", default="auto", choices=("auto", "z", "y"),
                     help="c4/c5: split axis of the volume over the ranks (auto: less halo work)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling split of the frame")
+    ap.add_argument("--no-parity-sample", action="store_true", help="skip the oracle check of one output crop")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
                     help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
     args = ap.parse_args()
@@ -544,18 +681,40 @@ def main():
 
     # sanity: finite outputs
     finite = bool(torch.isfinite(d_vx).all().item())
+    kernels = set(plan.kernels())
+    plan.close()
+    ms_step = elapsed / args.steps * 1e3
+
+    # N > 1: the same frame split over the ranks (strong scaling, halo exchange over RCCL):
+    # z-slabs (the north star's axis) and the axis with less halo work (row slabs here)
+    strong = None
+    if world > 1 and not args.no_strong:
+        from opticalflow3d_dev_amd.shard import slab_axis
+
+        axes = [0] + ([1] if slab_axis(nz, ny, world, rd, rw) == 1 else [])
+        strong = {}
+        for ax in axes:
+            if world > (nz, ny)[ax]:
+                continue
+            r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step)
+            strong["zslab" if ax == 0 else "yslab"] = r
 
     if rank == 0:
-        ms_step = elapsed / args.steps * 1e3
         value = world * vox * args.steps / elapsed / 1e6
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
                         args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox,
-                        frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv, used=set(plan.kernels()))
-        cpu = None
+                        frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv, used=kernels)
+        cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             sub = min(cpu_sample_planes(nz, ny, nx, args.cpu_budget), nz)
             host = d_in[:, :sub].cpu().numpy().view(np.uint16)
             cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
+        if not args.no_parity_sample:
+            # one 16^3 output crop across the kernels' seams (K5c / K12 z chunk 64, K34 row chunk
+            # 256 at c3) against the oracle, outside the timed region
+            zc, yc, xc = min(64, nz // 2), min(256, ny // 2), nx // 2 + 44
+            box = (zc - 8, zc + 8, yc - 8, yc + 8, min(xc, nx - 16), min(xc, nx - 16) + 16)
+            parity = parity_sample(d_in, (d_vx, d_vy, d_vz, d_rel), box, s, t, w, fp32)
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
@@ -565,9 +724,12 @@ def main():
                        "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
                        "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite},
             "roofline": roof, "cpu_baseline": cpu,
+            "parity_sample": parity, "build": build_stamp(),
         }
+        if strong is not None:
+            line["strong"] = dict(strong, note="the same frame split over the ranks (halo exchange over "
+                                               "RCCL P2P beside compute); value = frame voxels / step time")
         print(json.dumps(line), flush=True)
-    plan.close()
     if world > 1:
         dist.destroy_process_group()
 

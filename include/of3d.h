@@ -84,6 +84,13 @@ typedef struct of3d_plan of3d_plan;
 /* Library version (OF3D_VERSION). */
 int of3d_version(void);
 
+/* Build provenance, a JSON object: {"src_hash": sha256 (first 16 hex digits) of the sources
+ * the library was compiled from (csrc/Makefile HASH_FILES), "arch", "extra": the EXTRA
+ * compile flags (empty for a product build), "flags"}.  The Python loader compares src_hash
+ * with the sources beside the library and refuses a stale or EXTRA-flagged build.  No
+ * reference counterpart (the reference has no compiled code). */
+const char* of3d_build_info(void);
+
 /* Last error message of the calling thread ("" if none). */
 const char* of3d_last_error(void);
 
@@ -165,7 +172,8 @@ int of3d_plan_stage_times(of3d_plan* plan, double* ms, int cap);
  * solve stages of chunk c on the plan's second stream (joined back into the
  * caller's stream before the call's work completes).  Results are bit-identical
  * to the serial order.  A per-stage profile (timing mask with several stages)
- * runs serially; with one timed stage its time is summed over the chunks. */
+ * runs serially; with one timed stage its time is summed over the chunks.  Fails while the
+ * plan has an output row range (of3d_plan_set_rows), as set_rows fails on a chunked plan. */
 int of3d_plan_set_overlap(of3d_plan* plan, int64_t chunk_planes);
 
 /* Output rows (3D plans with the fused products/W-xy and W-z kernels): of3d_plan_execute

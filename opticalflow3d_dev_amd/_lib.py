@@ -38,8 +38,62 @@ EXPORTED = (
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
-    "of3d_plan_kernels",
+    "of3d_plan_kernels", "of3d_build_info",
 )
+
+CSRC = os.path.join(_HERE, "csrc")
+INCLUDE_H = os.path.join(os.path.dirname(_HERE), "include", "of3d.h")
+
+
+def source_hash() -> str | None:
+    """sha256 (16 hex digits) of the library's sources, concatenated in csrc/Makefile's
+    HASH_FILES order (sorted *.hip / *.hpp, Makefile, include/of3d.h); None when the
+    sources are not beside the package."""
+    import glob
+    import hashlib
+
+    files = sorted(os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(
+        os.path.join(CSRC, "*.hpp")))
+    paths = [os.path.join(CSRC, f) for f in files] + [os.path.join(CSRC, "Makefile"), INCLUDE_H]
+    if not files or not all(os.path.exists(p) for p in paths):
+        return None
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """of3d_build_info() of the loaded library, plus the hash of the sources beside it."""
+    import json
+
+    info = json.loads(load().of3d_build_info().decode())
+    info["tree_hash"] = source_hash()
+    info["lib"] = os.path.relpath(LIB_PATH, os.path.dirname(_HERE))
+    return info
+
+
+def _check_provenance(lib):
+    """Refuse a library built from other sources than the tree's, or with EXTRA flags (an
+    A/B experiment build): OF3D_ALLOW_STALE=1 loads it anyway, with a warning."""
+    import json
+    import warnings
+
+    info = json.loads(lib.of3d_build_info().decode())
+    tree = source_hash()
+    problems = []
+    if tree is not None and info.get("src_hash") != tree:
+        problems.append(f"built from sources {info.get('src_hash')}, tree has {tree} (rebuild: make -C "
+                        "opticalflow3d_dev_amd/csrc)")
+    if info.get("extra"):
+        problems.append(f"built with EXTRA flags {info['extra']!r} (experiment build)")
+    if problems:
+        msg = f"opticalflow3d_dev_amd: {LIB_PATH}: " + "; ".join(problems)
+        if os.environ.get("OF3D_ALLOW_STALE") == "1":
+            warnings.warn(msg + " [loaded: OF3D_ALLOW_STALE=1]")
+        else:
+            raise ImportError(msg)
 
 
 class Taps(ctypes.Structure):
@@ -83,6 +137,10 @@ def load():
         except ImportError:
             pass
         lib = ctypes.CDLL(LIB_PATH)
+        if not hasattr(lib, "of3d_build_info"):
+            raise ImportError(f"opticalflow3d_dev_amd: {LIB_PATH} predates build provenance; rebuild it")
+        lib.of3d_build_info.restype = ctypes.c_char_p
+        _check_provenance(lib)
         P = ctypes.c_void_p
         D = ctypes.POINTER(ctypes.c_double)
         F = ctypes.POINTER(ctypes.c_float)

@@ -204,7 +204,8 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     rows of every plane (less halo work when Ny >> Nz: the y pass is the first pass of
     both filter chains).  ``"auto"``: frames when there are at least as many output
     frames as ranks, else the slab axis with less predicted halo work
-    (shard.slab_axis).  Files and pixel values are the same as on one GPU."""
+    (shard.slab_axis).  A slab split that would leave a rank without planes (rows) runs
+    as frames instead.  Files and pixel values are the same as on one GPU."""
     ### Check Inputs and Set Up Paths (calc_flow.py:413-442)
     imDir = Path(imDir)
     if not imDir.is_dir():
@@ -275,13 +276,19 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     names = ('vx', 'vy', 'vz', 'rel') if spatialDimensions == 3 else ('vx', 'vy', 'rel')
     flow = calc_flow3D if spatialDimensions == 3 else calc_flow2D
 
+    allImages = None
     if fileType == 'OneTif':
         try:
             allImages = tf.memmap(imDir / (imName + '.tif'))
-        except ValueError:  # compressed / tiled / scattered pages: decoded into memory
-            allImages = tf.imread(imDir / (imName + '.tif'))
-        load_frame = lambda i: allImages[i]
-        load_planes = lambda i, z0, z1: np.asarray(allImages[i][z0:z1])
+        except ValueError:  # compressed / tiled / scattered pages: each call decodes only its pages
+            one = tf.TiffFile(imDir / (imName + '.tif'))
+            npg = int(Nz) if spatialDimensions == 3 else 1  # frame i plane z = page i * Nz + z (ImageJ TZYX)
+            load_frame = (lambda i: one.read_planes(i * npg, (i + 1) * npg)) if spatialDimensions == 3 else \
+                (lambda i: one.read_planes(i, i + 1)[0])
+            load_planes = lambda i, z0, z1: one.read_planes(i * npg + z0, i * npg + z1)
+        if allImages is not None:
+            load_frame = lambda i: allImages[i]
+            load_planes = lambda i, z0, z1: np.asarray(allImages[i][z0:z1])
     else:
         load_frame = lambda i: tf.imread(imDir / fileList[i])
         load_planes = lambda i, z0, z1: tf.TiffFile(imDir / fileList[i]).read_planes(z0, z1)
@@ -305,9 +312,13 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
 
         rd_, _, _, rw_ = radii(xyzSig, tSig, wSig)
         axis = slab_axis(int(Nz), int(Ny), world, rd_, rw_)
+    if axis is not None and world > (int(Nz), int(Ny))[axis]:
+        axis = None  # a slab per rank would leave ranks empty (shard.check_slab_split): split frames
     if axis is not None:
-        if fileType == 'OneTif':
+        if fileType == 'OneTif' and allImages is not None:
             load_rows = lambda i, y0, y1: np.asarray(allImages[i][:, y0:y1])
+        elif fileType == 'OneTif':
+            load_rows = lambda i, y0, y1: load_frame(i)[:, y0:y1]
         else:
             load_rows = lambda i, y0, y1: tf.TiffFile(imDir / fileList[i]).read_rows(y0, y1)
         _process_slab(load_planes if axis == 0 else load_rows, axis, (int(Nz), int(Ny), int(Nx)), nOut, NtChunk,

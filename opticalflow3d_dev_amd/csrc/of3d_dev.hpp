@@ -857,12 +857,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
             const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
             if (sg >= nseg) continue;
             F out[RB];
-#ifndef OF3D_EXP_NOB
             lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
-#else  // experiment: phase B without its pass (one LDS read per output)
-#pragma unroll
-            for (int e = 0; e < RB; ++e) out[e] = tile[k34_row(r, cwp) + RW + RB * sg + e];
-#endif
             if (r < nr) {
                 // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
                 const int c0 = RB * sg;
@@ -902,7 +897,6 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
                                 rb[ic1 % PD] = buf_ld<F>(rb_, vof, o1);
                                 F a0 = ring[(j + RW) % NR] * h[0];
                                 F a1 = ring[(j + 1 + RW) % NR] * h[0];
-#ifndef OF3D_EXP_NOA
                                 a0 = a0 + (ring[j % NR] + ring[(j + 2 * RW) % NR]) * h[RW];
                                 a1 = a1 + (ring[(j + 1) % NR] + ring[(j + 1 + 2 * RW) % NR]) * h[RW];
                                 ring[ic1 % NR] = p1;  // slot of row j - RW (NR = 2 RW + 2): free now
@@ -911,9 +905,6 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
                                     a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
                                     a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
                                 }
-#else
-                                ring[ic1 % NR] = p1;
-#endif
                                 put(tile + k34_row(j % S, cwp), a0);
                                 put(tile + k34_row((j + 1) % S, cwp), a1);
                             }(),
@@ -937,7 +928,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // arithmetic instead of alternating in lockstep.  One barrier per tile, two tile buffers:
 // producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
 // k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
-// Ablation at c3 (OF3D_EXP_K34_NOST / OF3D_EXP_K34_L2, timing only): without the W-xy
+// Ablation at c3 (round 2, timing-only experiment builds since removed): without the W-xy
 // stores 1.13 ms (the VALU ideal at the measured clock) vs 1.72; gradient loads from one
 // cache-resident row 1.48.  Staging the stores through a wave-private LDS transpose (whole
 // rows per store instruction) measured slower (1.88 ms): the 72 B/voxel W-xy hand-off to
@@ -1022,11 +1013,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
         constexpr unsigned long long pb = NP == 9 ? 0x313231000ull : 0x12100ull;
         const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
         const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
-#ifndef OF3D_EXP_K34_L2
         auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
-#else  // experiment (timing only): every gradient load from one row (cache-resident)
-        auto rowoff = [&](int idx) { return (unsigned)clampi(y0 + (idx & 1), 0, ny - 1) * rowb; };
-#endif
         F ring[NR], ra[PD], rb[PD];
 #pragma unroll
         for (int i = 0; i <= 2 * RW; ++i) {
@@ -1101,11 +1088,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                 if (sg >= nseg) continue;
                 F out[RB];
                 lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
-#ifndef OF3D_EXP_K34_NOST
                 if (r < nr) {
-#else  // experiment (timing only): no W-xy stores
-                if (r < nr && out[0] == (F)1.2345e-30) {
-#endif
                     const int c0 = RB * sg;
                     const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
                     if (c0 + RB <= txu) {
@@ -1601,9 +1584,6 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 // Needs nx * sizeof(F) and nx * sizeof(T) multiples of 16 bytes and 16-byte aligned planes.
 // ---------------------------------------------------------------------------
 constexpr int K12_TY = 4;  // rows per block
-#ifndef OF3D_K12_EXP
-#define OF3D_K12_EXP 0  // experiments: 1 = no gradient stores, 2 = no chunk waits (timing only)
-#endif
 template <int RD>
 __host__ __device__ constexpr int k12_tx() { return 128 - 2 * RD; }
 // LDS bytes of one staged plane: NRW rows of dt0 (128 + EPL columns) and of I (128 + EPL_T)
@@ -1768,9 +1748,7 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                     constexpr int j = J;
                     const int s = u0 + j;
                     const bool chunk_end = s % K == K - 1;
-#if OF3D_K12_EXP != 2
                     if (chunk_end) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
                     lds_barrier();
                     if (chunk_end) {
                         const int m2 = s / K + 2;
@@ -1824,15 +1802,11 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                             o1 = o1 + (r1[slotz(cz - k, NR)] + r1[slotz(cz + k, NR)]) * hg[k];
                             o4 = o4 + (r4[slotz(cz - k, NR)] - r4[slotz(cz + k, NR)]) * hd[k];
                         }
-#if OF3D_K12_EXP != 1
                         if (st_ok) {
                             const size_t pq = (size_t)(q - zg0) * plane;
                             buf_st<F>(o1, buf_rsrc(G + pq), vout, sout);
                             buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vout, sout);
                         }
-#else
-                        if (o1 == 12345.0 && o4 == 1.0) G[0] = 0;
-#endif
                     }
                     if (s >= RD + RS && s < nout + RD + RS) {  // plane q = qa + s - RD - RS: dy and dx
                         const int q = qa + s - RD - RS;
@@ -1843,15 +1817,11 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                             o2 = o2 + (r2[slotz(cz - k, NRS)] + r2[slotz(cz + k, NRS)]) * hs[k];
                             o3 = o3 + (r3[slotz(cz - k, NRS)] + r3[slotz(cz + k, NRS)]) * hs[k];
                         }
-#if OF3D_K12_EXP != 1
                         if (st_ok) {
                             const size_t pq = (size_t)(q - zg0) * plane;
                             buf_st<F>(o2, buf_rsrc(G + fs + pq), vout, sout);
                             buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vout, sout);
                         }
-#else
-                        if (o2 == 12345.0 && o3 == 1.0) G[1] = 0;
-#endif
                     }
                     if (s + 1 >= nsteps) done = true;
                 }(),
@@ -2147,35 +2117,15 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
-#ifndef OF3D_EXP_K5_NOPASS
         lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
-#else  // experiment: no W-z arithmetic (one LDS read per output)
-#pragma unroll
-        for (int i = 0; i < R; ++i) acc[f][i] = sm[(f % NB) * HG * RPWI * CB + col + (RW + gz * R + i) * CB];
-#endif
         // pin the pass here: without it the compiler sinks every field's arithmetic below the
         // last barrier and keeps all 9 windows' LDS reads live in registers (spills)
 #pragma unroll
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
     if (x >= nx) return;
-#ifndef OF3D_EXP_K5_NOSOLVE
     k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
                                vy, vz, rel);
-#else  // experiment: no solve / eigenvalue (stores the field sums)
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        if (zc0 + gz * R - zo0 + i >= nzo) break;
-        F a = acc[0][i];
-#pragma unroll
-        for (int f = 1; f < 9; ++f) a = a + acc[f][i];
-        const size_t o = (size_t)(zc0 + gz * R - zo0 + i) * gridDim.y * nx + (size_t)kb.by * nx + x;
-        vx[o] = a;
-        vy[o] = a;
-        vz[o] = a;
-        rel[o] = (RelT)a;
-    }
-#endif
 }
 // K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
 // float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each

@@ -1051,7 +1051,13 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     OF3D_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
     for (auto& e : p->ev_chunk) OF3D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char* e = getenv("OF3D_ZCHUNK")) p->zchunk = atoll(e);
-    if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
+    // OF3D_K34_CAND=i pins the i-th candidate geometry of the K34 autotune (tests run every
+    // candidate and compare bits; multi-rank runs can pin one choice for every rank)
+    if (const char* e = getenv("OF3D_K34_CAND"); e && e[0]) {
+        const size_t i = (size_t)atoll(e);
+        if (i >= p->k34_cand.size()) return fail("of3d: OF3D_K34_CAND out of range");
+        p->k34 = p->k34_cand[i];
+    } else if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
         OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
         OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
         if ((p->fp32 ? k34_tune<float>(p.get()) : k34_tune<double>(p.get()))) return -1;
@@ -1391,6 +1397,9 @@ int of3d_plan_kernels(const of3d_plan* p, char* buf, size_t n) {
 
 int of3d_plan_set_overlap(of3d_plan* p, int64_t chunk_planes) {
     if (!p) return fail("of3d: null plan");
+    // the two modes exclude each other both ways (of3d_plan_set_rows refuses a chunked plan)
+    if (chunk_planes > 0 && (p->ya != 0 || p->yb != p->ny))
+        return fail("of3d: overlap mode needs the full row range (of3d_plan_set_rows(0, ny) first)");
     p->zchunk = chunk_planes > 0 ? chunk_planes : 0;
     return 0;
 }

@@ -6,16 +6,17 @@ Two ways the path shards, both one process per GPU (process_flow picks one per r
    calc_flow.py:512: "this could become a parfor loop").  Rank r takes output
    frames r, r+P, ...; no collective on the data path.
 
-2. z-slabs of one large frame — rank p owns output planes [z0_p, z1_p).  Every
-   stage clamps at the GLOBAL volume edge (scipy mode='nearest' on the whole
-   volume), so a slab computed from input planes [z0-H, z1+H) ∩ [0, Nz) with
-   H = rd + rw (gradient z-pass radius + window z-pass radius) is bit-identical
-   to the same planes of the unsharded result.  The plan reports the exact
-   input range (of3d_plan_input_range).  When the input stack is already
-   distributed across GPUs (each rank holds its own planes), the halo planes
-   come from the z-neighbours: ``exchange_halos`` sends/receives them with
-   torch.distributed point-to-point (RCCL over xGMI for CUDA tensors, gloo for
-   CPU tensors) — the only collective on this path.
+2. Slabs of one large frame — rank p owns output planes [z0_p, z1_p) (or rows, the
+   same way).  Every stage clamps at the GLOBAL volume edge (scipy mode='nearest' on
+   the whole volume), so a slab computed from input planes [z0-H, z1+H) ∩ [0, Nz) with
+   H = rd + rw (gradient z-pass radius + window z-pass radius) is bit-identical to the
+   same planes of the unsharded result.  The plan reports the exact input range
+   (of3d_plan_input_range).  Each rank reads only its own planes of every frame; the
+   halo planes come from the neighbours: ``exchange_frame_halo`` (one frame per output
+   frame, stream.FlowStream(zslab=...)) sends/receives them with torch.distributed
+   point-to-point (RCCL over xGMI for CUDA tensors, gloo staged through host memory) —
+   the only collective on this path.  Every rank must own at least one plane (row):
+   ``check_slab_split`` refuses thinner splits (process_flow then splits frames).
 """
 
 from __future__ import annotations
@@ -147,6 +148,15 @@ def exchange_frame_halo(block, zi0: int, z0: int, z1: int, nz: int, halo: int, r
         t.copy_(buf)
 
 
+def check_slab_split(n_axis: int, world: int) -> None:
+    """Slab splits give every rank at least one plane (row) of the split axis: a rank with an
+    empty slab would take no part in the halo exchange's P2P batches (RCCL needs every rank
+    of the communicator in its first batch) and hold a zero-size plan."""
+    if world > n_axis:
+        raise ValueError(f"slab split of {n_axis} planes over {world} ranks leaves empty slabs "
+                         "(at most one rank per plane; split frames instead)")
+
+
 def zslab_bounds(nz: int, rank: int, world: int) -> tuple:
     """Balanced contiguous output planes [z0, z1) of rank `rank` (may be empty when world > nz)."""
     base, extra = divmod(nz, world)
@@ -171,157 +181,6 @@ def _bytes(t):
     return t.reshape(-1).view(torch.uint8)
 
 
-def exchange_halos(local, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
-    """Assemble the input planes [max(z0-halo,0), min(z1+halo,nz)) of this rank.
-
-    ``local``: tensor (..., z1-z0, Ny, Nx) — this rank's own planes on axis -3
-    (CPU tensors over gloo, CUDA tensors over RCCL).  Neighbour planes are
-    exchanged with batched point-to-point ops; ranks at the global edge get
-    nothing from outside (the kernels clamp there).  Slabs thinner than the
-    halo pull from several ranks.  Returns (tensor, zi0)."""
-    import torch
-    import torch.distributed as dist
-
-    zi0, zi1 = max(z0 - halo, 0), min(z1 + halo, nz)
-    bounds = [zslab_bounds(nz, r, world) for r in range(world)]
-    ops, recv = [], {}
-    for r in range(world):
-        if r == rank:
-            continue
-        rz0, rz1 = bounds[r]
-        # planes rank r needs from me
-        need0, need1 = max(rz0 - halo, 0), min(rz1 + halo, nz)
-        s0, s1 = max(need0, z0), min(need1, z1)
-        if s1 > s0:
-            send = local[..., s0 - z0:s1 - z0, :, :].contiguous()
-            ops.append(dist.P2POp(dist.isend, _bytes(send), r, group))
-        # planes I need from rank r
-        g0, g1 = max(zi0, rz0), min(zi1, rz1)
-        if g1 > g0:
-            shape = list(local.shape)
-            shape[-3] = g1 - g0
-            buf = torch.empty(shape, dtype=local.dtype, device=local.device)
-            recv[r] = (g0, g1, buf)
-            ops.append(dist.P2POp(dist.irecv, _bytes(buf), r, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    pieces = []
-    for r in range(world):
-        if r == rank:
-            pieces.append((z0, local))
-        elif r in recv:
-            pieces.append((recv[r][0], recv[r][2]))
-    pieces.sort(key=lambda t: t[0])
-    out = torch.cat([p for _, p in pieces if p.shape[-3] > 0], dim=-3)
-    assert out.shape[-3] == zi1 - zi0
-    return out, zi0
-
-
-class SlabRunner:
-    """Computes the output planes [z0, z1) of a 3D frame on one GPU from device-resident input planes.
-
-    frames: uint16/... device tensor (2*rt+1, zi1-zi0, Ny, Nx) holding planes [zi0, zi1)."""
-
-    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=0, timing=0, mode=0):
-        self.nz, self.ny, self.nx = nz, ny, nx
-        self.z0, self.z1 = z0, z1
-        self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
-        self.plan = _lib.Plan(3, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=device,
-                              max_out_planes=max(z1 - z0, 1), timing=timing, mode=mode)
-        self.zi0, self.zi1 = self.plan.input_range(z0, z1)
-
-    def run(self, frames, dtype_code, vx, vy, vz, rel, stream=0):
-        ptrs = [frames[i].data_ptr() for i in range(frames.shape[0])]
-        self.plan.execute(ptrs, dtype_code, self.zi0, self.z0, self.z1, vx.data_ptr(), vy.data_ptr(),
-                          vz.data_ptr(), rel.data_ptr(), stream)
-
-    def close(self):
-        self.plan.close()
-
-
-def fill_halos(block, zi0: int, z0: int, z1: int, nz: int, halo: int, rank: int, world: int, group=None):
-    """In-place form of exchange_halos: ``block`` (..., zi1-zi0, Ny, Nx) already
-    holds this rank's planes [z0, z1) at offset z0-zi0; the halo planes are
-    received from the neighbours into it (and this rank's boundary planes sent
-    from it).  Only halo-sized temporaries are allocated."""
-    import torch
-    import torch.distributed as dist
-
-    if world == 1:
-        return block
-    zi1 = zi0 + block.shape[-3]
-    # gloo moves host tensors only: stage CUDA planes through host memory there
-    stage = block.is_cuda and dist.get_backend(group) == "gloo"
-    bounds = [zslab_bounds(nz, r, world) for r in range(world)]
-    ops, recv = [], []
-    for r in range(world):
-        if r == rank:
-            continue
-        rz0, rz1 = bounds[r]
-        if rz1 <= rz0:
-            continue
-        need0, need1 = max(rz0 - halo, 0), min(rz1 + halo, nz)
-        s0, s1 = max(need0, z0), min(need1, z1)
-        if s1 > s0:
-            send = block[..., s0 - zi0:s1 - zi0, :, :].contiguous()
-            ops.append(dist.P2POp(dist.isend, _bytes(send.cpu() if stage else send), r, group))
-        g0, g1 = max(zi0, rz0), min(zi1, rz1)
-        if g1 > g0:
-            shape = list(block.shape)
-            shape[-3] = g1 - g0
-            buf = torch.empty(shape, dtype=block.dtype, device="cpu" if stage else block.device)
-            recv.append((g0, g1, buf))
-            ops.append(dist.P2POp(dist.irecv, _bytes(buf), r, group))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-    for g0, g1, buf in recv:
-        block[..., g0 - zi0:g1 - zi0, :, :].copy_(buf)
-    return block
-
-
-class ZSlabFlow:
-    """One rank's share of a z-sharded frame (SURVEY §8e, configs[3]).
-
-    Each rank holds only its own input planes [z0, z1) of the 2*rt+1 frames
-    (as it would after reading its z-range of the TIFF), written into
-    ``own`` — a view of the rank's input block [zi0, zi1).  run() fetches the
-    H = rd + rw halo planes from the z-neighbours with torch.distributed P2P
-    (RCCL over xGMI for CUDA tensors) into the block, then computes output
-    planes [z0, z1) — bit-identical to the unsharded frame.  Outputs stay on
-    this rank (no gather)."""
-
-    def __init__(self, nz, ny, nx, xyzSig, tSig, wSig, rank, world, device=0, timing=0, group=None, mode=0):
-        self.rank, self.world, self.group = rank, world, group
-        self.z0, self.z1 = zslab_bounds(nz, rank, world)
-        self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
-        self.halo = self.rd + self.rw
-        self.nz, self.ny, self.nx = nz, ny, nx
-        self.runner = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, self.z0, self.z1, device=device, timing=timing,
-                                 mode=mode) if self.z1 > self.z0 else None
-        self.zi0, self.zi1 = halo_planes(nz, self.z0, self.z1, self.rd, self.rw)
-        if self.runner is not None:
-            assert (self.runner.zi0, self.runner.zi1) == (self.zi0, self.zi1)
-        self.block = None
-
-    def allocate(self, dtype, device):
-        """Input block (2rt+1, zi1-zi0, ny, nx); returns the view of this rank's own planes."""
-        import torch
-
-        self.block = torch.empty((2 * self.rt + 1, self.zi1 - self.zi0, self.ny, self.nx), dtype=dtype, device=device)
-        return self.block[:, self.z0 - self.zi0:self.z1 - self.zi0]
-
-    def run(self, dtype_code, vx, vy, vz, rel, stream=0):
-        fill_halos(self.block, self.zi0, self.z0, self.z1, self.nz, self.halo, self.rank, self.world, self.group)
-        if self.runner is not None:
-            self.runner.run(self.block, dtype_code, vx, vy, vz, rel, stream)
-
-    def close(self):
-        if self.runner is not None:
-            self.runner.close()
-
-
 def flow3d_zslabs_host(images, xyzSig, tSig, wSig, world, device=0):
     """Reference-shaped helper: run calc_flow3D as `world` z-slabs on one device
     (virtual ranks) through device plans, concatenating the slabs.  Used to
@@ -340,15 +199,20 @@ def flow3d_zslabs_host(images, xyzSig, tSig, wSig, world, device=0):
         z0, z1 = zslab_bounds(nz, rank, world)
         if z1 <= z0:
             continue
-        sr = SlabRunner(nz, ny, nx, xyzSig, tSig, wSig, z0, z1, device=device)
-        part = np.ascontiguousarray(win[:, sr.zi0:sr.zi1])
-        t_in = torch.from_numpy(part.view(np.int16) if a.dtype == np.uint16 else part).to(dev)
-        n = (z1 - z0) * ny * nx
-        vx, vy, vz = (torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3))
-        rel = torch.empty(n, dtype=torch.float32, device=dev)
-        sr.run(t_in, code, vx, vy, vz, rel, torch.cuda.current_stream(dev).cuda_stream)
-        torch.cuda.synchronize(dev)
-        for o, t in zip(outs, (vx, vy, vz, rel)):
-            o[z0:z1] = t.cpu().numpy().reshape(z1 - z0, ny, nx)
-        sr.close()
+        plan = _lib.Plan(3, nz, ny, nx, make_taps(xyzSig, tSig, wSig), device=device, max_out_planes=z1 - z0)
+        try:
+            zi0, zi1 = plan.input_range(z0, z1)
+            assert (zi0, zi1) == halo_planes(nz, z0, z1, rd, rw)
+            part = np.ascontiguousarray(win[:, zi0:zi1])
+            t_in = torch.from_numpy(part.view(np.int16) if a.dtype == np.uint16 else part).to(dev)
+            n = (z1 - z0) * ny * nx
+            vx, vy, vz = (torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3))
+            rel = torch.empty(n, dtype=torch.float32, device=dev)
+            plan.execute([t_in[i].data_ptr() for i in range(t_in.shape[0])], code, zi0, z0, z1, vx.data_ptr(),
+                         vy.data_ptr(), vz.data_ptr(), rel.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+            torch.cuda.synchronize(dev)
+            for o, t in zip(outs, (vx, vy, vz, rel)):
+                o[z0:z1] = t.cpu().numpy().reshape(z1 - z0, ny, nx)
+        finally:
+            plan.close()
     return tuple(outs)

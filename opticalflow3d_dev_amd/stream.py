@@ -60,7 +60,7 @@ class FlowStream:
         exact: bit-identical), and keep the own rows."""
         import torch
 
-        from .shard import halo_planes, zslab_bounds
+        from .shard import check_slab_split, halo_planes, zslab_bounds
 
         self.torch = torch
         self.ndim = ndim
@@ -83,6 +83,8 @@ class FlowStream:
             raise ValueError("z-slabs need a 3D volume")
         self.rank, self.world, self.group = zslab[:3] if zslab is not None else (0, 1, None)
         self.axis = zslab[3] if zslab is not None and len(zslab) > 3 else 0
+        if zslab is not None:
+            check_slab_split((nz, ny)[self.axis], self.world)  # every rank owns planes (rows)
         plane = ny * nx
         taps = make_taps(xyzSig, tSig, wSig)
         if precision not in ("fp64", "fp32"):

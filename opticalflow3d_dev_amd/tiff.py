@@ -227,11 +227,13 @@ class TiffFile:
         return any(p.compression != 1 or not p.offsets for p in self.pages)
 
     def read_planes(self, z0, z1):
-        """Pages [z0, z1) of a plain page series (a SequenceT time point), as (z1 - z0, y, x):
-        only those bytes are read when the pages are uncompressed."""
+        """Pages [z0, z1) of a plain page series (a SequenceT time point, or the planes of a
+        OneTif hyperstack: frame i plane z is page i * Nz + z), as (z1 - z0, y, x): only those
+        bytes are read when the pages are uncompressed, only those pages decoded otherwise."""
         p0 = self.pages[0]
         if self._needs_codec():
-            return np.ascontiguousarray(imread_libtiff(self.path).reshape((len(self.pages),) + p0.shape)[z0:z1])
+            arr = imread_libtiff(self.path, pages=(z0, z1)).reshape((z1 - z0,) + p0.shape)
+            return np.ascontiguousarray(arr, dtype=p0.dtype.newbyteorder("="))
         blk = self._contiguous_block()
         out = np.empty((z1 - z0,) + p0.shape, p0.dtype.newbyteorder("="))
         with open(self.path, "rb") as f:
@@ -508,6 +510,8 @@ def _libtiff():
         lib.TIFFWriteDirectory.restype = ctypes.c_int
         lib.TIFFReadDirectory.argtypes = [P]
         lib.TIFFReadDirectory.restype = ctypes.c_int
+        lib.TIFFSetDirectory.argtypes = [P, ctypes.c_uint32]
+        lib.TIFFSetDirectory.restype = ctypes.c_int
         lib.TIFFClose.argtypes = [P]
         lib.TIFFClose.restype = None
         lib.TIFFIsTiled.argtypes = [P]
@@ -591,19 +595,25 @@ def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, t
         lib.TIFFClose(tif)
 
 
-def imread_libtiff(path):
+def imread_libtiff(path, pages=None):
     """Read any single-sample TIFF libtiff can decode (e.g. the LZW BigTIFFs of
-    imwrite_matlab / MATLAB's TIFFwrite) as a (pages, y, x) or (y, x) array."""
+    imwrite_matlab / MATLAB's TIFFwrite) as a (pages, y, x) or (y, x) array.
+    pages=(p0, p1): decode only pages [p0, p1) (always a (p1 - p0, y, x) array)."""
     import ctypes
 
     lib = _libtiff()
     tif = lib.TIFFOpen(os.fsencode(str(path)), b"r")
     if not tif:
         raise OSError("libtiff could not open " + str(path))
+    if pages is not None:
+        p0, p1 = pages
+        if p1 <= p0 or not lib.TIFFSetDirectory(tif, p0):
+            lib.TIFFClose(tif)
+            raise ValueError(f"{path}: no pages [{p0}, {p1})")
     T = _TIFFTAG
     get = lambda tag, ct: (lambda v: (lib.TIFFGetField(ctypes.c_void_p(tif), ctypes.c_uint32(tag), ctypes.byref(v)),
                                       v.value)[1])(ct())
-    pages = []
+    planes = []
     try:
         while True:
             w, h = get(T["IMAGEWIDTH"], ctypes.c_uint32), get(T["IMAGELENGTH"], ctypes.c_uint32)
@@ -628,9 +638,13 @@ def imread_libtiff(path):
                         if n < 0:
                             raise OSError("libtiff failed decoding " + str(path))
                         out[ty:ty + th, tx:tx + tw] = tile[:min(th, h - ty), :min(tw, w - tx)]
-            pages.append(out)
-            if not lib.TIFFReadDirectory(tif):
+            planes.append(out)
+            if (pages is not None and len(planes) == pages[1] - pages[0]) or not lib.TIFFReadDirectory(tif):
                 break
     finally:
         lib.TIFFClose(tif)
-    return pages[0] if len(pages) == 1 else np.stack(pages)
+    if pages is not None:
+        if len(planes) != pages[1] - pages[0]:
+            raise ValueError(f"{path}: fewer than {pages[1]} pages")
+        return np.stack(planes)
+    return planes[0] if len(planes) == 1 else np.stack(planes)

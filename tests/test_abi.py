@@ -40,3 +40,12 @@ def test_null_plan_is_an_error_not_a_crash():
     assert "null" in _lib.last_error()
     a, b = ctypes.c_int64(), ctypes.c_int64()
     assert lib.of3d_plan_input_range(None, 0, 1, ctypes.byref(a), ctypes.byref(b)) != 0
+
+
+def test_build_provenance_matches_tree():
+    """of3d_build_info: the library was built from exactly the sources in the tree, with no
+    EXTRA (experiment) flags — the loader refuses anything else (OF3D_ALLOW_STALE aside)."""
+    info = _lib.build_info()
+    assert info["src_hash"] == info["tree_hash"] == _lib.source_hash()
+    assert info["extra"] == "" and info["arch"] == "gfx950"
+    assert "-ffp-contract=off" in info["flags"]

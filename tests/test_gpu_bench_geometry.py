@@ -1,0 +1,217 @@
+"""The benchmarked geometry pinned to the oracle: bench.py's headline workload (configs[2],
+c3: 19 x 128 x 512 x 512, xyzSig 2, tSig 3, wSig 7, fp64) run through the same Plan the
+bench times, on the bench's own synthetic input, compared with the oracle
+(oracle/cpu_ref.py, pinned to the reference's calc_flow3D, calc_flow.py:175-360) on crops.
+
+Crops: an output voxel further than rd + rw = 6 + 21 = 27 voxels from every face where the
+crop cuts the volume sees no clamping the full volume does not (the y, x, z gradient passes
+reach rd, the W passes rw further), so the oracle of the crop's input box gives its exact
+outputs.  The crops cover the seams of the kernels' decompositions at this size: K12's and
+K5c's 64-plane z chunks (plane 64, where K5c's XCD block remap is live: 2 z chunks), K34's
+256-row chunks (row 256), and the volume corners and x edge (global clamping).
+
+Every kernel family the plan can pick at this size (the K34 autotune's candidates, the
+duplicate / unique / wave-specialised K34 forms, K5c's 4- and 8-wave blocks, K1c + K2c
+instead of K12) is forced in turn and must give the same bits.
+
+Tolerances: vx, vy, vz bitwise; rel within 1e-6 * lambda_max of the fp64
+eigenvalue; fp32 plans within 1e-4 * max|v| of the fp64 oracle.
+"""
+import contextlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_rel_within, bits_equal, oracle3d
+
+pytestmark = pytest.mark.gpu
+
+C3 = dict(nt=19, nz=128, ny=512, nx=512, s=2, t=3, w=7)
+HALO = 6 + 21  # rd + rw at xyzSig 2, wSig 7
+# output boxes (z0, z1, y0, y1, x0, x1)
+CROPS = {
+    "z64_y256_interior": (52, 76, 244, 268, 300, 330),
+    "corner_origin": (0, 20, 0, 24, 0, 24),
+    "corner_far": (108, 128, 488, 512, 486, 512),
+    "x_edge_y256": (30, 48, 248, 264, 0, 28),
+}
+
+
+@contextlib.contextmanager
+def env(**kv):
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def run_plan(d_in, nz, ny, nx, s, t, w, mode=0):
+    """One output frame through a device plan as bench.py runs it: (vx, vy, vz, rel) device
+    tensors and the kernel families the plan launched."""
+    import torch
+
+    from opticalflow3d_dev_amd import _lib, make_taps
+
+    dev = d_in.device
+    fp32 = bool(mode & _lib.OF3D_FP32)
+    n = nz * ny * nx
+    vt = torch.float32 if fp32 else torch.float64
+    outs = [torch.full((n,), float("nan"), dtype=vt, device=dev) for _ in range(3)]
+    outs.append(torch.full((n,), float("nan"), dtype=torch.float32, device=dev))
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=dev.index, timing=4, mode=mode)
+    try:
+        plan.execute([d_in[i].data_ptr() for i in range(d_in.shape[0])], _lib.OF3D_U16, 0, 0, nz,
+                     *[o.data_ptr() for o in outs], torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        kernels = plan.kernels()
+    finally:
+        plan.close()
+    return [o.view(nz, ny, nx) for o in outs], kernels
+
+
+def same_bits(a, b):
+    import torch
+
+    it = torch.int64 if a.element_size() == 8 else torch.int32
+    return a.shape == b.shape and a.dtype == b.dtype and bool(torch.equal(a.view(it), b.view(it)))
+
+
+def crop_check(host_in, outs, box, s, t, w, fp32=False):
+    """Oracle of the crop's input box vs the outputs in `box` (host copies of the crop only)."""
+    nt, nz, ny, nx = host_in.shape
+    z0, z1, y0, y1, x0, x1 = box
+    lo = [max(a - HALO, 0) for a in (z0, y0, x0)]
+    hi = [min(b + HALO, n) for b, n in zip((z1, y1, x1), (nz, ny, nx))]
+    sub = np.ascontiguousarray(host_in[:, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]])
+    vx, vy, vz, lmin, lmax = oracle3d(sub, s, t, w)
+    sl = (slice(z0 - lo[0], z1 - lo[0]), slice(y0 - lo[1], y1 - lo[1]), slice(x0 - lo[2], x1 - lo[2]))
+    got = [o[z0:z1, y0:y1, x0:x1].cpu().numpy() for o in outs]
+    if fp32:
+        for g, want in zip(got[:3], (vx[sl], vy[sl], vz[sl])):
+            assert np.abs(g.astype(np.float64) - want).max() <= 1e-4 * np.abs(want).max()
+        assert np.abs(got[3].astype(np.float64) - lmin[sl]).max() <= 1e-4 * np.abs(lmax[sl]).max()
+        return
+    for g, want, name in zip(got[:3], (vx[sl], vy[sl], vz[sl]), ("vx", "vy", "vz")):
+        assert bits_equal(g, want), (box, name)
+    assert_rel_within(got[3], lmin[sl], lmax[sl], 1e-6)
+
+
+@pytest.fixture(scope="module")
+def c3():
+    """bench.py's c3 input (synthetic_slab, seed 20260206 + 3 as bench.main uses at rank 0),
+    resident on the device, and the default plan's outputs."""
+    import torch
+
+    import bench
+    from opticalflow3d_dev_amd import radii
+
+    p = C3
+    rt = radii(p["s"], p["t"], p["w"])[2]
+    dev = torch.device("cuda", 0)
+    d_in = bench.synthetic_slab(2 * rt + 1, p["nz"], p["ny"], p["nx"], 0, p["nz"], 20260206 + 3, dev)
+    outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"])
+    host_in = d_in.cpu().numpy().view(np.uint16)
+    yield d_in, host_in, outs, kernels
+    del d_in, outs
+    torch.cuda.empty_cache()
+
+
+def test_c3_default_plan_kernels(c3):
+    """The headline plan runs the fused kernels the bench's roofline names."""
+    _, _, outs, kernels = c3
+    assert "k_grad_xyz_c" in kernels and "k_wz_solve_c" in kernels, kernels
+    assert any(k.startswith("k_prod_wyx") for k in kernels), kernels
+    for o in outs[:3]:
+        assert bool(o.isfinite().all())
+
+
+@pytest.mark.parametrize("crop", sorted(CROPS))
+def test_c3_full_size_vs_oracle_crops(c3, crop):
+    d_in, host_in, outs, _ = c3
+    crop_check(host_in, outs, CROPS[crop], C3["s"], C3["t"], C3["w"])
+
+
+def k34_candidates(d_in, p, mode=0):
+    """Number of K34 autotune candidates of this plan shape (OF3D_K34_CAND past the end fails)."""
+    from opticalflow3d_dev_amd import _lib, make_taps
+
+    n = 0
+    while n < 64:
+        with env(OF3D_K34_CAND=n):
+            try:
+                _lib.Plan(3, p["nz"], p["ny"], p["nx"], make_taps(p["s"], p["t"], p["w"]), device=0,
+                          mode=mode).close()
+            except RuntimeError as e:
+                assert "OF3D_K34_CAND out of range" in str(e)
+                return n
+        n += 1
+    return n
+
+
+FAMILIES = [dict(OF3D_K34_UQ=0), dict(OF3D_K34_UQ=1), dict(OF3D_K34_UQ=2), dict(OF3D_K5C_NW=8),
+            dict(OF3D_K5C_R=4), dict(OF3D_K12=0), dict(OF3D_K34_TUNE=0)]
+
+
+def test_c3_every_kernel_family_bit_identical(c3):
+    """Each forced family and each K34 autotune candidate at the headline size gives the
+    default plan's bits (so the timing-based autotune cannot change a result)."""
+    d_in, _, ref, _ = c3
+    p = C3
+    ncand = k34_candidates(d_in, p)
+    assert ncand >= 2
+    variants = FAMILIES + [dict(OF3D_K34_CAND=i) for i in range(ncand)]
+    seen = set()
+    for v in variants:
+        with env(**v):
+            outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"])
+        seen.update(kernels)
+        for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
+            assert same_bits(a, b), (v, name, kernels)
+        del outs
+    # the families really changed: lockstep, wave-specialised K34, K1c + K2c, 8-wave K5c
+    assert {"k_prod_wyx", "k_prod_wyx_ws", "k_grad_xy_c", "k_grad_z_c"} <= seen, seen
+
+
+def test_c3_fp32_plans_vs_oracle_and_candidates(c3):
+    """configs[4]'s fp32 path at the c3 size: every K34 candidate (packed, wave-specialised,
+    lockstep fp32 kernels) bit-identical, and the outputs within 1e-4 of the fp64 oracle."""
+    from opticalflow3d_dev_amd import _lib
+
+    d_in, host_in, _, _ = c3
+    p = C3
+    mode = _lib.OF3D_FP32
+    ref, _ = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+    ncand = k34_candidates(d_in, p, mode)
+    for v in [dict(OF3D_K34_CAND=i) for i in range(ncand)] + [dict(OF3D_K12=0), dict(OF3D_K5C_PK=1)]:
+        with env(**v):
+            outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+        for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
+            assert same_bits(a, b), (v, name, kernels)
+        del outs
+    crop_check(host_in, ref, CROPS["z64_y256_interior"], p["s"], p["t"], p["w"], fp32=True)
+    crop_check(host_in, ref, CROPS["corner_far"], p["s"], p["t"], p["w"], fp32=True)
+
+
+@pytest.mark.parametrize("variant", [dict(), dict(OF3D_K5C_NW=8), dict(OF3D_K34_UQ=0), dict(OF3D_K34_UQ=2),
+                                     dict(OF3D_K12=1)])
+def test_more_than_64_planes_small_xy_vs_oracle(variant):
+    """13 x 200 x 41 x 48 (sigma 2, tau 2, omega 5): four K5c z chunks, and a block grid whose
+    size is not a multiple of 8 z-chunk sets, so the XCD remap's tail branch runs
+    (csrc/of3d_dev.hpp k5c_block); the whole volume against the oracle."""
+    import torch
+
+    img = np.random.default_rng(64).integers(0, 4096, size=(13, 200, 41, 48)).astype(np.uint16)
+    d_in = torch.from_numpy(np.ascontiguousarray(img[6 - 6:6 + 7]).view(np.int16)).to("cuda")
+    with env(**variant):
+        outs, kernels = run_plan(d_in, 200, 41, 48, 2, 2, 5)
+    vx, vy, vz, lmin, lmax = oracle3d(img, 2, 2, 5)
+    for g, want, name in zip(outs[:3], (vx, vy, vz), ("vx", "vy", "vz")):
+        assert bits_equal(g.cpu().numpy(), want), (variant, name, kernels)
+    assert_rel_within(outs[3].cpu().numpy(), lmin, lmax, 1e-6)

@@ -83,6 +83,47 @@ def test_onetif_multi_rank_equals_single(tmp_path, world, parallel, shape):
         assert_flow3d_matches_oracle(got, stack[hh:hh + 7], 1, 1, 2)
 
 
+@pytest.mark.parametrize("world,parallel", [(2, "zslab"), (3, "zslab"), (2, "yslab"), (3, "yslab"), (2, "frames")])
+def test_fp32_multi_rank_equals_single_and_oracle(tmp_path, world, parallel):
+    """configs[4]: process_flow(precision="fp32") split over ranks (slabs with the halo
+    exchange, or frames) writes the same float32 files, byte for byte, as one process, and
+    their pixels are within 1e-4 of the oracle's fp64 flow (calc_flow.py:507-534)."""
+    from oracle import cpu_ref
+    from test_gpu_process_flow import assert_fp32_flow_close
+
+    stack = cpu_ref.synthetic_stack_np((8, 12, 30, 24), seed=30 + world)
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    for d in (single, multi):
+        d.mkdir()
+        tf.imwrite(d / "c.tif", stack, imagej=True)
+    process_flow(str(single), "c", "OneTif", 3, 1, 1, 2, precision="fp32")
+    _run_ranks(world, (str(multi), "c", "OneTif", 3, 1, 1, 2), {"parallel": parallel, "precision": "fp32"})
+    a, b = _tree(single / "OpticalFlow3D"), _tree(multi / "OpticalFlow3D")
+    assert sorted(a) == sorted(b) and len(a) == 1 + 4 * 2
+    for k in a:
+        assert a[k] == b[k], k
+    out = multi / "OpticalFlow3D" / "c"
+    for hh in range(2):
+        got = [tf.imread(out / f"c_{n}_t{hh + 3:04d}.tiff") for n in ("vx", "vy", "vz", "rel")]
+        assert_fp32_flow_close(got, stack[hh:hh + 7], 1, 1, 2)
+
+
+def test_slab_split_wider_than_volume_runs_frames(tmp_path):
+    """parallel="zslab" with more ranks than planes: no empty slabs (shard.check_slab_split),
+    the run falls back to frame blocks and writes the single-process files."""
+    stack = np.random.default_rng(12).integers(0, 4096, size=(9, 2, 16, 20)).astype(np.uint16)
+    single, multi = tmp_path / "single", tmp_path / "multi"
+    for d in (single, multi):
+        d.mkdir()
+        tf.imwrite(d / "e.tif", stack, imagej=True)
+    process_flow(str(single), "e", "OneTif", 3, 1, 1, 2)
+    _run_ranks(3, (str(multi), "e", "OneTif", 3, 1, 1, 2), {"parallel": "zslab"})
+    a, b = _tree(single / "OpticalFlow3D"), _tree(multi / "OpticalFlow3D")
+    assert sorted(a) == sorted(b)
+    for k in a:
+        assert a[k] == b[k], k
+
+
 def test_sequencet_zslab_three_ranks(tmp_path):
     stack = np.random.default_rng(5).integers(0, 4096, size=(8, 9, 14, 18)).astype(np.uint16)
     for t in range(8):
@@ -120,6 +161,21 @@ def test_sequencet_yslab_two_ranks(tmp_path):
     _run_ranks(2, (str(tmp_path), "r_t.*", "SequenceT", 3, 1, 1, 2), {"parallel": "yslab"})
     out = tmp_path / "OpticalFlow3D" / "r_t"
     got = [tf.imread(out / f"r_t_{n}_t0003.tiff") for n in ("vx", "vy", "vz", "rel")]
+    assert_flow3d_matches_oracle(got, stack, 1, 1, 2)
+
+
+@pytest.mark.parametrize("world,parallel", [(1, "auto"), (2, "zslab"), (2, "yslab")])
+def test_lzw_onetif_multi_rank(tmp_path, world, parallel):
+    """An LZW-compressed hyperstack split over ranks: every rank decodes only the pages of
+    its planes (tiff.imread_libtiff page ranges), results equal the oracle."""
+    stack = np.random.default_rng(16).integers(0, 4096, size=(7, 6, 18, 22)).astype(np.uint16)
+    tf.imwrite_libtiff(tmp_path / "q.tif", stack.reshape(-1, 18, 22), compression=5, bigtiff=False,
+                       description=tf.imagej_description(stack.shape))
+    if world == 1:
+        process_flow(str(tmp_path), "q", "OneTif", 3, 1, 1, 2)
+    else:
+        _run_ranks(world, (str(tmp_path), "q", "OneTif", 3, 1, 1, 2), {"parallel": parallel})
+    got = [tf.imread(tmp_path / "OpticalFlow3D" / "q" / f"q_{n}_t0003.tiff") for n in ("vx", "vy", "vz", "rel")]
     assert_flow3d_matches_oracle(got, stack, 1, 1, 2)
 
 

@@ -8,9 +8,6 @@ Tolerances:
   * fp32 path: max|dv| <= 1e-4 * max|v_ref| against the reference's fp64
     vx/vy/vz; rel within 1e-4 * max|rel_ref| (float32 tensor, fp64 solve).
 """
-import multiprocessing as mp
-import socket
-
 import numpy as np
 import pytest
 
@@ -46,55 +43,17 @@ def test_zslabs_seeded_vs_oracle(world):
     assert_flow3d_matches_oracle(out, img, 2, 2, 5)
 
 
-def _zslab_worker(rank, world, port, q, img, sig):
-    import os
-
-    import torch
-    import torch.distributed as dist
-
-    from opticalflow3d_dev_amd.shard import ZSlabFlow
-
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        nt, nz, ny, nx = img.shape
-        dev = torch.device("cuda", 0)
-        zf = ZSlabFlow(nz, ny, nx, *sig, rank, world, device=0)
-        own = zf.allocate(torch.int16, dev)
-        c, rt = nt // 2, zf.rt
-        own.copy_(torch.from_numpy(np.ascontiguousarray(img[c - rt:c + rt + 1, zf.z0:zf.z1]).view(np.int16)))
-        n = (zf.z1 - zf.z0) * ny * nx
-        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
-        rel = torch.empty(n, dtype=torch.float32, device=dev)
-        zf.run(_lib.OF3D_U16, *outs, rel, torch.cuda.current_stream(dev).cuda_stream)
-        torch.cuda.synchronize(dev)
-        q.put((rank, zf.z0, zf.z1, [t.cpu().numpy() for t in outs + [rel]]))
-        zf.close()
-    finally:
-        dist.destroy_process_group()
-
-
 def test_zslab_gloo_two_ranks_vs_oracle():
-    """Two real processes, each holding only its own planes and exchanging
-    halos over gloo: the union of the slabs equals the oracle bit for bit."""
+    """Two real processes on the product slab path (FlowStream(zslab=...)), each holding only
+    its own planes and exchanging halos over gloo: the union of the slabs equals the oracle
+    bit for bit."""
+    from test_gpu_shard import run_stream_slabs
+
     img = np.random.default_rng(9).integers(0, 4096, size=(13, 36, 24, 28)).astype(np.uint16)
     sig = (2, 2, 5)
     vx, vy, vz, lmin, lmax = oracle3d(img, *sig)
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_zslab_worker, args=(r, 2, port, q, img, sig)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = [q.get(timeout=180) for _ in range(2)]
-    for p in procs:
-        p.join(timeout=60)
     covered = 0
-    for rank, z0, z1, outs in res:
+    for rank, z0, z1, outs in run_stream_slabs(2, img, sig, 0):
         covered += z1 - z0
         shp = (z1 - z0, 24, 28)
         for got, want in zip(outs[:3], (vx, vy, vz)):
@@ -143,3 +102,26 @@ def test_fp32_3d_vs_oracle(shape, sig):
     vx, vy, vz, lmin, lmax = oracle3d(img, *sig)
     got = calc_flow3D_fp32(img, *sig)
     _assert_fp32_close(got, (vx, vy, vz), lmin)
+
+
+@pytest.mark.parametrize("world,axis", [(2, 0), (3, 0), (2, 1), (3, 1)])
+def test_fp32_slab_ranks_vs_oracle(world, axis):
+    """configs[4]'s fp32 path split over ranks (FlowStream(zslab=..., precision="fp32"),
+    gloo): every rank's part within 1e-4 * max|v| of the oracle's fp64 flow, and equal bit
+    for bit to the same part of the one-process fp32 result (slabs never change a bit)."""
+    from test_gpu_shard import run_stream_slabs
+
+    img = _smooth((13, 18, 40, 36), 5)
+    sig = (2, 2, 5)
+    vx, vy, vz, lmin, lmax = oracle3d(img, *sig)
+    one = calc_flow3D_fp32(img, *sig)
+    covered = 0
+    for rank, a0, a1, outs in run_stream_slabs(world, img, sig, axis, precision="fp32"):
+        covered += a1 - a0
+        cut = (lambda a: a[a0:a1]) if axis == 0 else (lambda a: a[:, a0:a1])
+        shp = cut(vx).shape
+        got = [o.reshape(shp) for o in outs]
+        _assert_fp32_close(got, (cut(vx), cut(vy), cut(vz)), cut(lmin))
+        for a, b in zip(one, got):
+            assert bits_equal(cut(a), b)
+    assert covered == (18, 40)[axis]

@@ -80,3 +80,36 @@ def test_overlap_one_stage_timing():
     img = np.random.default_rng(6).integers(0, 4096, size=(13, 40, 32, 64)).astype(np.uint16)
     out, times = _run_plan(img, s, t, w, 10, timing_stage="prod_wy")
     assert set(times) == {"prod_wy"} and times["prod_wy"] > 0
+
+
+@pytest.mark.parametrize("chunk", [8, 13])
+def test_overlap_with_k12_forced(monkeypatch, chunk):
+    """Overlap mode on the fused gradient kernel (K12 forced below its size heuristic: dt0
+    lives in Y4 there, the plane ranges of the two streams must still be disjoint): bitwise
+    equal to the serial pipeline and to the oracle."""
+    monkeypatch.setenv("OF3D_K12", "1")
+    s, t, w = 2, 2, 5
+    img = np.random.default_rng(70 + chunk).integers(0, 4096, size=(13, 48, 40, 56)).astype(np.uint16)
+    serial, _ = _run_plan(img, s, t, w, 0)
+    over, _ = _run_plan(img, s, t, w, chunk)
+    for a, b in zip(serial, over):
+        assert bits_equal(a, b)
+    st = cpu_ref.structure_tensor3d(img, s, t, w, backend="scipy")
+    for a, b in zip(over[:3], cpu_ref.solve3d(st)):
+        assert bits_equal(a, b)
+
+
+def test_overlap_and_row_range_exclude_each_other():
+    """of3d_plan_set_overlap fails on a plan with an output row range, and set_rows on a
+    chunked plan (the combination is not implemented)."""
+    plan = _lib.Plan(3, 24, 40, 48, make_taps(2, 2, 5), device=0)
+    try:
+        plan.set_rows(5, 30)
+        with pytest.raises(RuntimeError, match="row range"):
+            plan.set_overlap(8)
+        plan.set_rows(0, 40)
+        plan.set_overlap(8)
+        with pytest.raises(RuntimeError):
+            plan.set_rows(5, 30)
+    finally:
+        plan.close()

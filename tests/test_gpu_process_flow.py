@@ -100,9 +100,15 @@ def test_flowstream_ring_wraps(ndim, dtype, d2h):
 
 
 def _check_stream(p, win, ndim, tsig):
-    """One ring output against the oracle of its window."""
+    """One ring output against the oracle of its window, and bit for bit (rel included)
+    against the host entry point calc_flow3D / calc_flow2D of the same window."""
+    from opticalflow3d_dev_amd import calc_flow2D, calc_flow3D
+
     got = p.result()
     win = np.asarray(win).astype(np.asarray(win).dtype.newbyteorder("="))
+    direct = (calc_flow3D if ndim == 3 else calc_flow2D)(win, 1, tsig, 2)
+    for g, d in zip(got, direct):
+        assert bits_equal(g, d)
     if ndim == 3:
         assert_flow3d_matches_oracle(got, win, 1, tsig, 2)
     else:
@@ -166,3 +172,43 @@ def test_matlab_output_mode(tmp_path):
     for g, want in zip(got[:3], (vx, vy, vz)):
         assert bits_equal(g, want)
     assert_rel_within(got[3], lmin, lmax, 1e-10)  # fp64 rel vs fp64 eigvalsh
+
+
+FP32_TOL = 1e-4
+
+
+def assert_fp32_flow_close(got, images, s, t, w):
+    """fp32 outputs within 1e-4 * max|v| of the oracle's fp64 flow (rel: of max|lambda_max|)."""
+    from conftest import oracle3d
+
+    vx, vy, vz, lmin, lmax = oracle3d(images, s, t, w)
+    for g, want in zip(got[:3], (vx, vy, vz)):
+        assert g.dtype == np.float32 and g.shape == want.shape
+        assert np.abs(g.astype(np.float64) - want).max() <= FP32_TOL * np.abs(want).max()
+    assert np.abs(got[3].astype(np.float64) - lmin).max() <= FP32_TOL * np.abs(lmax).max()
+
+
+@pytest.mark.parametrize("fileType", ["OneTif", "SequenceT"])
+def test_process_flow_fp32_vs_oracle(tmp_path, fileType):
+    """configs[4]'s product entry, process_flow(..., precision="fp32") (calc_flow.py:507-534's
+    loop on the fp32 path): float32 TIFFs whose pixels are within 1e-4 of the oracle's fp64
+    flow of each window."""
+    from opticalflow3d_dev_amd.calc_flow import calc_flow3D_fp32
+
+    stack = cpu_ref.synthetic_stack_np((9, 10, 24, 28), seed=21)
+    if fileType == "OneTif":
+        tf.imwrite(tmp_path / "f.tif", stack, imagej=True)
+        name = "f"
+    else:
+        for t in range(9):
+            tf.imwrite(tmp_path / f"f_t{t}.tif", stack[t])
+        name = "f_t.*"
+    process_flow(str(tmp_path), name, fileType, 3, 1, 1, 2, precision="fp32")
+    save = name.replace(".*", "")
+    out = tmp_path / "OpticalFlow3D" / save
+    for hh in range(3):
+        got = [tf.imread(out / f"{save}_{n}_t{hh + 3:04d}.tiff") for n in ("vx", "vy", "vz", "rel")]
+        assert all(g.dtype == np.float32 for g in got)
+        assert_fp32_flow_close(got, stack[hh:hh + 7], 1, 1, 2)
+        for g, d in zip(got, calc_flow3D_fp32(stack[hh:hh + 7], 1, 1, 2)):
+            assert bits_equal(g, d)  # the ring path = the one-shot fp32 entry, bit for bit

@@ -31,63 +31,76 @@ def test_plan_input_range_matches_python():
     plan.close()
 
 
-def _zslab_worker(rank, world, port, q):
+def stream_slab_worker(rank, world, port, q, img, sig, axis, precision="fp64"):
+    """One rank of a slab split on the product path: FlowStream(zslab=(rank, world, group,
+    axis)) holds only the rank's planes (axis 0) or rows (axis 1) of every frame, fetches the
+    halo with shard.exchange_frame_halo (gloo here, all ranks on the one GPU; RCCL on a
+    node), and returns the rank's part of vx, vy, vz, rel."""
     import os
 
-    import torch
     import torch.distributed as dist
 
-    from opticalflow3d_dev_amd.shard import ZSlabFlow
+    from opticalflow3d_dev_amd.shard import zslab_bounds
+    from opticalflow3d_dev_amd.stream import FlowStream
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        img = np.random.default_rng(7).integers(0, 4096, size=(13, 30, 20, 24)).astype(np.uint16)
-        dev = torch.device("cuda", 0)
-        zf = ZSlabFlow(30, 20, 24, 2, 2, 5, rank, world, device=0)
-        own = zf.allocate(torch.int16, dev)
-        own.copy_(torch.from_numpy(img[:, zf.z0:zf.z1].view(np.int16)))
-        n = (zf.z1 - zf.z0) * 20 * 24
-        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(3)]
-        rel = torch.empty(n, dtype=torch.float32, device=dev)
-        zf.run(_lib.OF3D_U16, *outs, rel, torch.cuda.current_stream(dev).cuda_stream)
-        torch.cuda.synchronize(dev)
-        q.put((rank, zf.z0, zf.z1, [t.cpu().numpy() for t in outs + [rel]]))
-        zf.close()
+        nt, nz, ny, nx = img.shape
+        a0, a1 = zslab_bounds((nz, ny)[axis], rank, world)
+        fs = FlowStream(3, (nz, ny, nx), img.dtype, *sig, device=0, depth=1, precision=precision,
+                        zslab=(rank, world, None, axis))
+        try:
+            rt = fs.rt
+            c = nt // 2
+            for k in range(c - rt, c + rt + 1):
+                fs.push(img[k, a0:a1] if axis == 0 else img[k, :, a0:a1])
+            pend = fs.submit()
+            outs = [o.copy() for o in pend.result()]
+            pend.release()
+        finally:
+            fs.close()
+        q.put((rank, a0, a1, outs))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_zslab_ranks_with_halo_exchange(world):
-    """ZSlabFlow as bench.py's c4 path runs it: each rank holds only its own
-    planes, fetches halos from its neighbours (gloo here, staged through host
-    memory; RCCL on a multi-GPU node), and its slab equals the same planes of
-    the unsharded frame bit for bit."""
+def run_stream_slabs(world, img, sig, axis, precision="fp64"):
+    """stream_slab_worker on `world` spawned processes; [(rank, a0, a1, outs)] by rank."""
     import multiprocessing as mp
     import socket
 
-    img = np.random.default_rng(7).integers(0, 4096, size=(13, 30, 20, 24)).astype(np.uint16)
-    full = calc_flow3D(img, 2, 2, 5)
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_zslab_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=stream_slab_worker, args=(r, world, port, q, img, sig, axis, precision))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=180) for _ in range(world)]
+    res = sorted(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("world,axis", [(2, 0), (3, 0), (2, 1), (3, 1)])
+def test_slab_ranks_with_halo_exchange(world, axis):
+    """The product slab path (FlowStream(zslab=...) + exchange_frame_halo, as process_flow and
+    bench.py's slab configs run it): each rank's part equals the same planes / rows of the
+    unsharded frame bit for bit."""
+    img = np.random.default_rng(7).integers(0, 4096, size=(13, 30, 20, 24)).astype(np.uint16)
+    full = calc_flow3D(img, 2, 2, 5)
     covered = 0
-    for rank, z0, z1, outs in res:
-        covered += z1 - z0
+    for rank, a0, a1, outs in run_stream_slabs(world, img, (2, 2, 5), axis):
+        covered += a1 - a0
         for a, b in zip(full, outs):
-            assert bits_equal(a[z0:z1], b.reshape(z1 - z0, 20, 24))
-    assert covered == 30
+            want = a[a0:a1] if axis == 0 else a[:, a0:a1]
+            assert bits_equal(want, b.reshape(want.shape)), (rank, axis)
+    assert covered == (30, 20)[axis]
 
 
 @pytest.mark.parametrize("rows", [(0, 60), (7, 41), (0, 1), (59, 60), (13, 14)])

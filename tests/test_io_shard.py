@@ -47,7 +47,13 @@ def test_compressed_onetif_reads(tmp_path, compression):
     assert t.imagej_metadata["frames"] == 6 and t.imagej_metadata["slices"] == 5
     assert np.array_equal(t.asarray(), a)
     with pytest.raises(ValueError):
-        tf.memmap(tmp_path / "c.tif")  # process_flow falls back to imread
+        tf.memmap(tmp_path / "c.tif")  # process_flow falls back to page-range decodes
+    # frame i plane z = page i * Nz + z: a frame's planes / a slab's planes, decoded alone
+    for i, z0, z1 in ((0, 0, 5), (3, 1, 4), (5, 4, 5)):
+        assert np.array_equal(t.read_planes(i * 5 + z0, i * 5 + z1), a[i, z0:z1])
+    assert np.array_equal(tf.imread_libtiff(tmp_path / "c.tif", pages=(29, 30)), a[5, 4:5])
+    with pytest.raises(ValueError):
+        tf.imread_libtiff(tmp_path / "c.tif", pages=(28, 31))
 
 
 def test_tiled_and_page_ranges(tmp_path):

@@ -9,7 +9,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from opticalflow3d_dev_amd.shard import exchange_halos, frame_assignment, halo_planes, zslab_bounds, fill_halos
+from opticalflow3d_dev_amd.shard import (check_slab_split, exchange_frame_halo, frame_assignment, halo_planes,
+                                         halo_transfers, zslab_bounds)
 
 
 @pytest.mark.parametrize("nz,world", [(64, 1), (64, 2), (64, 3), (7, 8), (256, 4), (5, 5), (1, 2)])
@@ -42,28 +43,42 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, nz, halo, q):
+def _frame_halo_worker(rank, world, port, nz, halo, axis, q):
+    """A time series of frames through exchange_frame_halo, as FlowStream(zslab=...) runs it:
+    each rank's block holds only its own planes (rows) of every frame, then receives the
+    halo; afterwards it equals the global frame over the rank's input range."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        full = torch.arange(3 * nz * 4 * 5, dtype=torch.int32).reshape(3, nz, 4, 5)
-        z0, z1 = zslab_bounds(nz, rank, world)
-        local = full[:, z0:z1].contiguous()
-        got, zi0 = exchange_halos(local, z0, z1, nz, halo, rank, world)
-        zi1 = min(z1 + halo, nz)
-        ok = zi0 == max(z0 - halo, 0) and torch.equal(got, full[:, zi0:zi1])
-        q.put((rank, bool(ok)))
+        ok = True
+        for frame in range(3):
+            full = (torch.arange(nz * 4 * 5, dtype=torch.int16) + 1000 * frame).reshape(nz, 4, 5)
+            if axis == 1:  # rows first, the block a strided view (row slabs)
+                full = full.reshape(4, nz, 5).transpose(0, 1)
+            z0, z1 = zslab_bounds(nz, rank, world)
+            zi0, zi1 = max(z0 - halo, 0), min(z1 + halo, nz)
+            if axis == 0:
+                block = torch.full((zi1 - zi0, 4, 5), -1, dtype=torch.int16)
+            else:
+                block = torch.full((4, zi1 - zi0, 5), -1, dtype=torch.int16).transpose(0, 1)
+            block[z0 - zi0:z1 - zi0] = full[z0:z1]
+            exchange_frame_halo(block, zi0, z0, z1, nz, halo, rank, world)
+            ok = ok and bool(torch.equal(block, full[zi0:zi1]))
+        q.put((rank, ok))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nz,halo", [(2, 16, 3), (3, 10, 4), (4, 6, 3), (2, 5, 21)])
-def test_exchange_halos_gloo(world, nz, halo):
+@pytest.mark.parametrize("world,nz,halo,axis", [(2, 16, 3, 0), (3, 10, 4, 0), (4, 6, 3, 0), (2, 5, 21, 0),
+                                                (3, 9, 27, 0), (2, 16, 3, 1), (3, 11, 5, 1), (4, 4, 2, 1)])
+def test_exchange_frame_halo_gloo(world, nz, halo, axis):
+    """The product halo exchange (shard.exchange_frame_halo): z-slabs (contiguous planes) and
+    row slabs (strided rows through temporaries), slabs thinner than the halo included."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, nz, halo, q)) for r in range(world)]
+    procs = [ctx.Process(target=_frame_halo_worker, args=(r, world, port, nz, halo, axis, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -72,33 +87,18 @@ def test_exchange_halos_gloo(world, nz, halo):
     assert all(res[r] for r in range(world)), res
 
 
-def _fill_worker(rank, world, port, nz, rd, rw, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        full = torch.arange(3 * nz * 4 * 5, dtype=torch.int16).reshape(3, nz, 4, 5)
-        z0, z1 = zslab_bounds(nz, rank, world)
-        zi0, zi1 = halo_planes(nz, z0, z1, rd, rw)
-        block = torch.full((3, zi1 - zi0, 4, 5), -1, dtype=torch.int16)
-        block[:, z0 - zi0:z1 - zi0] = full[:, z0:z1]
-        fill_halos(block, zi0, z0, z1, nz, rd + rw, rank, world)
-        q.put((rank, bool(torch.equal(block, full[:, zi0:zi1]))))
-    finally:
-        dist.destroy_process_group()
+def test_slab_split_refuses_empty_slabs():
+    check_slab_split(8, 8)
+    check_slab_split(512, 8)
+    with pytest.raises(ValueError, match="empty slabs"):
+        check_slab_split(3, 4)
 
 
-@pytest.mark.parametrize("world,nz,rd,rw", [(2, 16, 1, 2), (3, 20, 2, 3), (4, 9, 1, 3), (4, 3, 1, 1), (2, 64, 6, 15)])
-def test_fill_halos_gloo(world, nz, rd, rw):
-    """In-place halo fill used by ZSlabFlow (bench.py c4): every rank's block
-    equals the global stack over [zi0, zi1), including empty slabs (world > nz)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_fill_worker, args=(r, world, port, nz, rd, rw, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-    assert all(res[r] for r in range(world)), res
+@pytest.mark.parametrize("nz,world,halo", [(64, 2, 27), (64, 8, 27), (9, 3, 27), (256, 4, 21)])
+def test_halo_transfers_symmetric(nz, world, halo):
+    """Every planned send has the matching receive on the peer (same planes)."""
+    sends = {r: halo_transfers(nz, r, world, halo)[0] for r in range(world)}
+    recvs = {r: halo_transfers(nz, r, world, halo)[1] for r in range(world)}
+    got = sorted((r, p, a, b) for r in range(world) for p, a, b in sends[r])
+    want = sorted((p, r, a, b) for r in range(world) for p, a, b in recvs[r])
+    assert got == want
