@@ -39,16 +39,38 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--d2h", default="dma", help="comma list of FlowStream download modes (dma,kernel,runtime)")
     ap.add_argument("--d2h-blocks", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=None,
+                    help="FlowStream output sets in flight (default 3; 1 for c5, whose workspace and ring take 215 GB)")
+    ap.add_argument("--precision", default=None, choices=("fp64", "fp32"),
+                    help="default: fp32 for c5 (configs[4]'s path), else fp64")
     args = ap.parse_args()
     nt0, nz, ny, nx, s, t, w, _ = CONFIGS[args.config]
+    precision = args.precision or ("fp32" if args.config == "c5" else "fp64")
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
     nt = nwin + args.frames - 1
     root = tempfile.mkdtemp(dir=args.dir)
     try:
-        stack = synthetic_frames(nt, nz, ny, nx, seed=0)
-        tf.imwrite(os.path.join(root, "series.tif"), stack, imagej=True)
         nvox = nz * ny * nx
+        t_gen = time.perf_counter()
+        if nvox * nt * 2 <= (8 << 30):
+            stack = synthetic_frames(nt, nz, ny, nx, seed=0)
+            tf.imwrite(os.path.join(root, "series.tif"), stack, imagej=True)
+            del stack
+        else:  # large configs: frames generated on the device, written page range by page range
+            import torch
+
+            from bench import synthetic_slab
+            for f in range(nt):
+                fr = synthetic_slab(1, nz, ny, nx, 0, nz, 20260206 + 7 + f, torch.device("cuda", 0))
+                tf.write_planes(os.path.join(root, "series.tif"), (nt, nz, ny, nx), np.uint16, f * nz,
+                                fr[0].cpu().numpy().view(np.uint16), imagej=True)
+                del fr
+                print(f"# wrote frame {f + 1}/{nt} ({time.perf_counter() - t_gen:.1f} s)", flush=True)
+            torch.cuda.empty_cache()
+        print(json.dumps({"input": "series.tif", "frames_in": nt, "bytes": nvox * nt * 2,
+                          "write_s": round(time.perf_counter() - t_gen, 2), "precision": precision}), flush=True)
+        out_es = 4 if precision == "fp32" else 8
         modes = []
         for m in args.modes.split(","):
             modes += [f"host:{d}" for d in args.d2h.split(",")] if m == "host" else [m]
@@ -59,7 +81,7 @@ def main():
             extra = {}
             if mode == "pcie":
                 import torch
-                d = torch.empty(nvox * 28 // 8, dtype=torch.float64, device="cuda")
+                d = torch.empty(nvox * (3 * out_es + 4) // 8, dtype=torch.float64, device="cuda")
                 h = torch.empty_like(d, device="cpu").pin_memory()
                 for direction in ("d2h", "h2d"):
                     src, dst = (d, h) if direction == "d2h" else (h, d)
@@ -75,7 +97,7 @@ def main():
                 from opticalflow3d_dev_amd import _lib
                 q = nvox * 8
                 for nsplit in (1, 4):
-                    parts = [q * 28 // 8 // nsplit] * nsplit
+                    parts = [q * (3 * out_es + 4) // 8 // nsplit] * nsplit
                     offs = [sum(parts[:i]) for i in range(nsplit)]
                     t0 = time.perf_counter()
                     for _ in range(10):
@@ -83,12 +105,15 @@ def main():
                     dt = time.perf_counter() - t0
                     print(json.dumps({"mode": f"dma_d2h_x{nsplit}", "GB_per_s": round(10 * sum(parts) / dt / 1e9, 2)}),
                           flush=True)
+                del d, h
+                torch.cuda.empty_cache()
                 continue
             if mode.startswith("host"):
                 from opticalflow3d_dev_amd.stream import FlowStream
                 mm = tf.memmap(os.path.join(root, "series.tif"))
                 fs = FlowStream(3, (nz, ny, nx), np.uint16, s, t, w, d2h=mode.split(":")[1],
-                                d2h_blocks=args.d2h_blocks)
+                                d2h_blocks=args.d2h_blocks, precision=precision,
+                                depth=args.depth or (1 if args.config == "c5" else 3))
                 split = {"push": 0.0, "submit": 0.0, "wait": 0.0}
                 for rep in range(2):  # rep 0 warms the plan (module load, workspace)
                     t0 = time.perf_counter()
@@ -135,9 +160,11 @@ def main():
                     extra.update({k: round(1e3 * v / fs.stats["dl_n"], 3) for k, v in fs.stats.items() if k != "dl_n"})
             elif mode == "stream":
                 with contextlib.redirect_stdout(io.StringIO()):
-                    process_flow(root, "series", "OneTif", 3, s, t, w)
+                    process_flow(root, "series", "OneTif", 3, s, t, w, precision=precision)
                 dt = time.perf_counter() - t0
             elif mode == "legacy":
+                if precision != "fp64":
+                    continue  # the reference's loop is the fp64 calc_flow3D
                 mm = tf.memmap(os.path.join(root, "series.tif"))
                 os.makedirs(out_dir, exist_ok=True)
                 for hh in range(args.frames):
@@ -152,7 +179,8 @@ def main():
                               "ms_per_frame": round(1e3 * dt / args.frames, 3),
                               "frames_per_s": round(args.frames / dt, 3),
                               "mvox_per_s": round(args.frames * nvox / dt / 1e6, 2),
-                              "out_bytes_per_frame": nvox * 28, **extra}), flush=True)
+                              "out_bytes_per_frame": nvox * (3 * out_es + 4), "precision": precision, **extra}),
+                  flush=True)
     finally:
         shutil.rmtree(root, ignore_errors=True)
 

@@ -14,9 +14,14 @@ i=0
 IFS=';' read -ra GRP <<< "$GROUPS_"
 for grp in "${GRP[@]}"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/pmc_${CFG}_$TAG/p$i" -o run \
-    -- python3 "$ROOT/bench.py" --config "$CFG" --steps "$STEPS" --warmup 1 --no-cpu-baseline > "$OUT/pmc_${CFG}_${TAG}_p$i.log" 2>&1
+  # counters only for this library's kernels (torch's input-generation kernels are many and small:
+  # collecting on each of them serialises minutes of launches at c5)
+  timeout -k 10 ${PASS_LIMIT:-240} rocprofv3 --pmc $grp --kernel-trace --kernel-include-regex "k_(tderiv|grad|prod|wz|solve)" \
+    --output-format csv -d "$OUT/pmc_${CFG}_$TAG/p$i" -o run \
+    -- python3 "$ROOT/bench.py" --config "$CFG" --steps "$STEPS" --warmup 1 --no-cpu-baseline --no-parity-sample > "$OUT/pmc_${CFG}_${TAG}_p$i.log" 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
+  # the dispatch traces are large (gpurun copies back at most 64 MiB): counters stay
+  find "$OUT/pmc_${CFG}_$TAG/p$i" -name "run_kernel_trace.csv" -delete 2>/dev/null
   case $rc in 0|1|2) ;; *) echo "STOP"; exit $rc;; esac
 done
 exit 0
