@@ -155,7 +155,7 @@ def fused_names(profile):
 # kernel families a plan reports (of3d_plan_kernels; kKernelNames in csrc/of3d_host.hip)
 PLAN_FAMILIES = {"k_tderiv_c", "k_tderiv", "k_grad_xy_c", "k_grad_xy", "k_grad_xyz_c", "k_grad_z_c", "k_grad_z",
                  "k_prod_wyx", "k_prod_wyx_ws", "k_prod_wy", "k_wx", "k_wz_solve_c", "k_wz_solve_c2",
-                 "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk"}
+                 "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk", "k_wz_solve_c_next"}
 
 
 def load_pmc_traffic(stage, cfg, used=None):
@@ -348,7 +348,8 @@ class SlabBench:
     compute) + the rank's compute.  vrank=(r, P): rank r of a P-way split on this one GPU,
     no exchange (the per-rank compute of the scaling model)."""
 
-    def __init__(self, dims, sig, axis, rank, world, dev, fp32=False, timing=0, vrank=None, seed=20260206):
+    def __init__(self, dims, sig, axis, rank, world, dev, fp32=False, timing=0, vrank=None, seed=20260206,
+                 pipeline=True):
         import torch
 
         from opticalflow3d_dev_amd import _lib, make_taps, radii
@@ -383,9 +384,12 @@ class SlabBench:
                     self.plan.set_rows(self.a0 - self.ai0, self.a1 - self.ai0)
                 except RuntimeError:
                     self.rows_direct = False
-        # 2 rt + 2 slots: the step's exchange goes to the slot the frame before last read
-        self.ring = torch.empty((self.nwin + 1,) + self.blk_shape, dtype=torch.int16, device=dev)
-        for f in range(self.nwin + 1):
+        # 2 rt + 2 slots (+ 1 with frame pipelining): the step's exchange goes to the slot the
+        # frame before last read
+        self.L = 1 if pipeline else 0
+        nslot = self.nwin + 1 + self.L
+        self.ring = torch.empty((nslot,) + self.blk_shape, dtype=torch.int16, device=dev)
+        for f in range(nslot):
             if axis == 0:
                 synthetic_slab(1, nz, ny, nx, self.ai0, self.ai1, seed + f, dev, out=self.ring[f:f + 1])
             else:
@@ -399,7 +403,8 @@ class SlabBench:
         self.comp = torch.cuda.current_stream(dev)
         self.xs = torch.cuda.Stream(device=dev)
         self.done = {}  # slot -> event of the last compute that read it
-        self.order = list(range(self.nwin))
+        self.xev = {}   # slot -> event of its frame's halo exchange (not yet waited for)
+        self.order = list(range(self.nwin + self.L))  # the window (+ the next window's newest frame)
 
     def _xchg_view(self, slot):
         v = self.ring[slot]
@@ -412,13 +417,16 @@ class SlabBench:
                             self.rank, self.world)
 
     def step(self, exchange=True, compute=True):
-        """The newest frame into the free slot (its halo exchanged on the side stream), then the
-        rank's compute on the compute stream behind it."""
+        """A new frame into the free slot (its halo exchanged on the side stream), and the
+        rank's compute of the current window on the compute stream.  Without pipelining the
+        new frame is the window's newest (the compute waits for its exchange); with it, the
+        new frame is the NEXT window's newest (exchanged one step ahead, beside this compute)
+        and this compute forms the next window's dt0 (of3d_plan_execute_next)."""
         import torch
 
         from opticalflow3d_dev_amd import _lib
 
-        new = (self.order[-1] + 1) % (self.nwin + 1)  # the free slot takes the newest frame
+        new = next(sl for sl in range(len(self.ring)) if sl not in self.order)  # the free slot
         if exchange and self.world > 1 and not self.vrank:
             with torch.cuda.stream(self.xs):
                 if new in self.done:
@@ -426,21 +434,31 @@ class SlabBench:
                 self.exchange(new)
                 ev = torch.cuda.Event()
                 ev.record(self.xs)
-            self.comp.wait_event(ev)
-        self.order.pop(0)
-        self.order.append(new)
-        if not compute:
-            return
-        ptrs = [self.ring[sl].data_ptr() for sl in self.order]
-        o = [t.data_ptr() for t in self.outs] + [self.rel.data_ptr()]
-        if self.axis == 0:
-            self.plan.execute(ptrs, _lib.OF3D_U16, self.ai0, self.a0, self.a1, *o, self.comp.cuda_stream)
-        else:
-            self.plan.execute(ptrs, _lib.OF3D_U16, 0, 0, self.dims[0], *o, self.comp.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(self.comp)
-        for sl in self.order:
-            self.done[sl] = ev
+            self.xev[new] = ev
+        if not self.L:
+            self.order.pop(0)
+            self.order.append(new)
+        for sl in self.order:  # the exchanges this compute reads
+            if sl in self.xev:
+                self.comp.wait_event(self.xev.pop(sl))
+        if compute:
+            window = self.order[:self.nwin]
+            ptrs = [self.ring[sl].data_ptr() for sl in window]
+            nxt = [self.ring[sl].data_ptr() for sl in self.order[1:]] if self.L else None
+            o = [t.data_ptr() for t in self.outs] + [self.rel.data_ptr()]
+            if self.axis == 0:
+                self.plan.execute(ptrs, _lib.OF3D_U16, self.ai0, self.a0, self.a1, *o, self.comp.cuda_stream,
+                                  next_ptrs=nxt, pipelined=bool(self.L))
+            else:
+                self.plan.execute(ptrs, _lib.OF3D_U16, 0, 0, self.dims[0], *o, self.comp.cuda_stream,
+                                  next_ptrs=nxt, pipelined=bool(self.L))
+            ev = torch.cuda.Event()
+            ev.record(self.comp)
+            for sl in self.order:
+                self.done[sl] = ev
+        if self.L:
+            self.order.pop(0)
+            self.order.append(new)
 
     def finite(self):
         return bool(self.outs[0][:self.n_out].isfinite().all().item()) if self.n_out else True
@@ -477,14 +495,14 @@ def timed_steps(step, steps, warmup, world, dev):
     return max_over_ranks([el], dev)[0] if world > 1 else el
 
 
-def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms):
+def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=True):
     """The default workload's frame split over the N ranks (strong scaling) — the path
     configs[3]/[4] and process_flow(parallel="zslab"/"yslab") run, on the headline volume:
     per-rank compute alone, the halo exchange alone (RCCL P2P of the newest frame's rd + rw
     planes / rows), and the pipelined step (exchange beside the previous step's compute).
     efficiency = the one-GPU frame time t1 (this run's replica step) / (N * step)."""
     nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
-    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50)
+    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50, pipeline=pipeline)
     try:
         comp = timed_steps(lambda: sb.step(exchange=False), steps, warmup, world, dev)
         xchg = timed_steps(lambda: sb.step(compute=False), steps, warmup, world, dev)
@@ -519,7 +537,7 @@ def run_slab(args, world, rank, local_rank, dev):
         axis = slab_axis(nz, ny, pworld, rd, rw)
     seed = 20260206 + (5 if fp32 else 4)
     sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32, timing=max(args.steps, 1),
-                   vrank=(prank, pworld) if vr else None, seed=seed)
+                   vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline)
     plan = sb.plan
     elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev)
     finite = sb.finite()
@@ -618,6 +636,8 @@ def main():
     ap.add_argument("--split", default="auto", choices=("auto", "z", "y"),
                     help="c4/c5: split axis of the volume over the ranks (auto: less halo work)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling split of the frame")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="no frame pipelining: every step launches its own K0 (of3d_plan_execute)")
     ap.add_argument("--no-parity-sample", action="store_true", help="skip the oracle check of one output crop")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
                     help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
@@ -671,9 +691,14 @@ def main():
     fptrs = [d_in[i].data_ptr() for i in range(nwin)]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
+    pipe = not args.no_pipeline
+
     def step():
+        # frame pipelining (of3d_plan_execute_next): this step's W-z/solve kernel also forms the
+        # next step's temporal derivative (the next frame of a series; here the same resident
+        # frames), so every timed step runs K12 + K34 + K5c-with-the-next-K0
         plan.execute(fptrs, _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(), d_vz.data_ptr(),
-                     d_rel.data_ptr(), stream)
+                     d_rel.data_ptr(), stream, next_ptrs=fptrs if pipe else None, pipelined=pipe)
 
     elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
     if world > 1:
@@ -696,7 +721,8 @@ def main():
         for ax in axes:
             if world > (nz, ny)[ax]:
                 continue
-            r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step)
+            r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step,
+                             pipeline=not args.no_pipeline)
             strong["zslab" if ax == 0 else "yslab"] = r
 
     if rank == 0:
@@ -722,7 +748,10 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32" if fp32 else "f64", "data": "synthetic",
             "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
                        "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
-                       "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite},
+                       "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite,
+                       "frame_pipelining": ("each step's W-z/solve kernel also forms the next step's temporal "
+                                            "derivative (of3d_plan_execute_next); stage grad_xy is then empty")
+                       if pipe else None},
             "roofline": roof, "cpu_baseline": cpu,
             "parity_sample": parity, "build": build_stamp(),
         }

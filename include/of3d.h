@@ -150,6 +150,19 @@ int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, i
                       int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz,
                       void* d_rel, void* stream);
 
+/* Frame pipelining for a time series (the reference's per-frame loop, calc_flow.py:512-534):
+ * of3d_plan_execute for d_frames, and — where the plan has the fused instance (uint16 frames,
+ * serial schedule) — the W-z/solve kernel of this call also forms the temporal derivative of
+ * the NEXT output frame from d_frames_next (2*rt+1 device pointers, same frame_z0 / planes;
+ * their contents must be final when this call is enqueued).  The next of3d_plan_execute_next
+ * call for exactly those frames and planes then skips its own K0 launch (a pure HBM stream
+ * riding in the VALU-bound kernel's memory slack).  d_frames_next NULL: no lookahead.  Any
+ * other call (of3d_plan_execute included) recomputes.  Results are bit-identical to
+ * of3d_plan_execute (the same K0 arithmetic, k0_group). */
+int of3d_plan_execute_next(of3d_plan* plan, const void* const* d_frames, const void* const* d_frames_next, int dtype,
+                           int64_t frame_z0, int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz,
+                           void* d_rel, void* stream);
+
 /* Per-stage timing with HIP events recorded on the launch stream.
  * of3d_plan_set_timing(plan, slots): keep a ring of `slots` executions
  * (0 = off; no host synchronisation is added to of3d_plan_execute).

@@ -38,7 +38,7 @@ EXPORTED = (
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
-    "of3d_plan_kernels", "of3d_build_info",
+    "of3d_plan_kernels", "of3d_build_info", "of3d_plan_execute_next",
 )
 
 CSRC = os.path.join(_HERE, "csrc")
@@ -166,6 +166,9 @@ def load():
         lib.of3d_plan_input_range.restype = ctypes.c_int
         lib.of3d_plan_execute.argtypes = [P, ctypes.POINTER(P), ctypes.c_int, i64, i64, i64, P, P, P, P, P]
         lib.of3d_plan_execute.restype = ctypes.c_int
+        lib.of3d_plan_execute_next.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.c_int, i64, i64, i64,
+                                               P, P, P, P, P]
+        lib.of3d_plan_execute_next.restype = ctypes.c_int
         lib.of3d_plan_stage_times.argtypes = [P, D, ctypes.c_int]
         lib.of3d_plan_stage_times.restype = ctypes.c_int
         lib.of3d_stage_name.argtypes = [ctypes.c_int]
@@ -263,10 +266,18 @@ class Plan:
         check(self.lib.of3d_plan_input_range(self.handle, z_out0, z_out1, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
-    def execute(self, frame_ptrs, dtype_code, frame_z0, z_out0, z_out1, vx, vy, vz, rel, stream=0):
+    def execute(self, frame_ptrs, dtype_code, frame_z0, z_out0, z_out1, vx, vy, vz, rel, stream=0,
+                next_ptrs=None, pipelined=False):
+        """of3d_plan_execute; pipelined=True: of3d_plan_execute_next (uses the dt0 the previous
+        pipelined call formed for these frames; with next_ptrs also forms the next frame's)."""
         arr = (ctypes.c_void_p * len(frame_ptrs))(*frame_ptrs)
-        check(self.lib.of3d_plan_execute(self.handle, arr, dtype_code, frame_z0, z_out0, z_out1,
-                                         vx, vy, vz, rel, stream or None))
+        if not pipelined and next_ptrs is None:
+            check(self.lib.of3d_plan_execute(self.handle, arr, dtype_code, frame_z0, z_out0, z_out1,
+                                             vx, vy, vz, rel, stream or None))
+            return
+        nxt = (ctypes.c_void_p * len(next_ptrs))(*next_ptrs) if next_ptrs is not None else None
+        check(self.lib.of3d_plan_execute_next(self.handle, arr, nxt, dtype_code, frame_z0, z_out0, z_out1,
+                                              vx, vy, vz, rel, stream or None))
 
     def stage_times(self):
         buf = (ctypes.c_double * 8)()

@@ -407,12 +407,15 @@ def _process_stream(load_frame, out_range, NtChunk, NtSlice, ndim, xyzSig, tSig,
     writer = Writer(finish)
     try:
         fs.push(first)
-        for i in range(h0 + 1, h0 + NtChunk - 1):
-            fs.push(load_frame(i))
+        pushed = h0 + 1  # next frame to upload
         for hh in range(h0, h1):
             start = datetime.now()
             start_str = str(start)
-            fs.push(load_frame(hh + NtChunk - 1))
+            # the window's frames, and (lookahead: frame pipelining) the next window's newest one
+            upto = hh + NtChunk + (1 if fs.lookahead and hh + 1 < h1 else 0)
+            while pushed < upto:
+                fs.push(load_frame(pushed))
+                pushed += 1
             writer.put(hh + NtSlice, start, start_str, fs.submit())
     finally:
         writer.close()

@@ -19,6 +19,6 @@ template <typename F, int NP> const void* k34_fn_ws(int rw, int s);         // k
 template <int NP> const void* k34_fn_pk(int rw, int s);                        // kt_prod.hip (packed fp32)
 template <typename F, typename RelT> const void* k5_kernel(int rw);          // kt_solve_legacy.hip
 template <typename F, typename RelT> const void* k5_dma_kernel(int rw, int nb);  // kt_solve_legacy.hip
-template <typename F, typename RelT> const void* k5c_fn(int rw, int nb, int r, int nw);  // kt_solve.hip
+template <typename F, typename RelT> const void* k5c_fn(int rw, int nb, int r, int nw, int rt0 = 0);  // kt_solve.hip
 template <typename RelT> const void* k5c2_fn(int rw, int nb, int r);            // kt_solve.hip (packed fp32)
 }  // namespace of3dk

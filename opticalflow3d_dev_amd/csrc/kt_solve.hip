@@ -5,8 +5,18 @@
 namespace of3dk {
 
 // K5c instances (window radii with a compiled pass, wSig 3..7; others use k_wz_solve_dma)
+// rt0 > 0: the instance that also forms the next frame's dt0 (uint16 frames; (rw, rt) of
+// configs[1..4]: (15, 6) and (21, 9))
 template <typename F, typename RelT>
-const void* k5c_fn(int rw, int nb, int r, int nw) {
+const void* k5c_fn(int rw, int nb, int r, int nw, int rt0) {
+    if (rt0 > 0) {
+        if (r != 8 || nw != 4) return nullptr;
+        if (rw == 21 && rt0 == 9)
+            return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, 21, 3, 8, 4, 9> : (const void*)k_wz_solve_c<F, RelT, 21, 2, 8, 4, 9>;
+        if (rw == 15 && rt0 == 6)
+            return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, 15, 3, 8, 4, 6> : (const void*)k_wz_solve_c<F, RelT, 15, 2, 8, 4, 6>;
+        return nullptr;
+    }
 #define OF3D_K5C(RW) \
     case RW:                                                                                            \
         if (nw == 8) return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, RW, 3, 8, 8> : nullptr;        \
@@ -47,9 +57,9 @@ const void* k5c2_fn(int rw, int nb, int r) {
 
 template const void* k5c2_fn<float>(int, int, int);
 template const void* k5c2_fn<double>(int, int, int);
-template const void* k5c_fn<double, float>(int, int, int, int);
-template const void* k5c_fn<double, double>(int, int, int, int);
-template const void* k5c_fn<float, float>(int, int, int, int);
-template const void* k5c_fn<float, double>(int, int, int, int);
+template const void* k5c_fn<double, float>(int, int, int, int, int);
+template const void* k5c_fn<double, double>(int, int, int, int, int);
+template const void* k5c_fn<float, float>(int, int, int, int, int);
+template const void* k5c_fn<float, double>(int, int, int, int, int);
 
 }  // namespace of3dk

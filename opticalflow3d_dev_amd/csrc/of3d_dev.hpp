@@ -281,42 +281,68 @@ __global__ __launch_bounds__(256) void k_tderiv_vec(Frames fr, size_t off0, size
 // K0 with a compile-time temporal radius: all 2RT+1 frame loads of a lane issued
 // before the first use (the runtime-rt loop above keeps only two in flight per lane:
 // latency-bound at 4.3 TB/s on c2).  Same arithmetic order.
+// One vector group of K0c: voxels o .. o + V - 1 of every frame -> D0g[0 .. V - 1] (shared by
+// the K0c kernel and the next-frame K0 inside the fused K5c, so both compute the same bits).
+template <typename T, typename F, int RT>
+__device__ __forceinline__ void k0_group_dt(const Frames& fr, size_t o, const F (&h)[RT + 1], F (&dt)[K0Vec<T>::V]) {
+    constexpr int V = K0Vec<T>::V, NW = 2 * RT + 1;
+    using Raw = typename std::conditional<K0Vec<T>::B == 8, unsigned long long, uint4>::type;
+    Raw raw[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) raw[i] = *reinterpret_cast<const Raw*>(reinterpret_cast<const T*>(fr.p[i]) + o);
+    auto val = [&](int i, int e) {
+        T t[V];
+        __builtin_memcpy(t, &raw[i], sizeof(Raw));
+        return (F)t[e];
+    };
+#pragma unroll
+    for (int e = 0; e < V; ++e) dt[e] = val(RT, e) * h[0];
+#pragma unroll
+    for (int k = RT; k >= 1; --k)
+#pragma unroll
+        for (int e = 0; e < V; ++e) dt[e] = dt[e] + (val(RT - k, e) - val(RT + k, e)) * h[k];
+}
+template <typename F, int V>
+__device__ __forceinline__ void k0_store(const F (&dt)[V], F* __restrict__ D0g) {
+    if constexpr (sizeof(F) == 8) {
+        double2* d = reinterpret_cast<double2*>(D0g);
+#pragma unroll
+        for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) D0g[i] = dt[i];
+    }
+}
+template <typename T, typename F, int RT>
+__device__ __forceinline__ void k0_group(const Frames& fr, size_t o, const F (&h)[RT + 1], F* __restrict__ D0g) {
+    F dt[K0Vec<T>::V];
+    k0_group_dt<T, F, RT>(fr, o, h, dt);
+    k0_store<F, K0Vec<T>::V>(dt, D0g);
+}
+
 template <typename T, typename F, int RT>
 __global__ __launch_bounds__(256) void k_tderiv_vec_c(Frames fr, size_t off0, size_t ngroups, const F* __restrict__ ht,
                                                       F* __restrict__ D0) {
-    constexpr int V = K0Vec<T>::V, NW = 2 * RT + 1;
-    using Raw = typename std::conditional<K0Vec<T>::B == 8, unsigned long long, uint4>::type;
+    constexpr int V = K0Vec<T>::V;
     F h[RT + 1];
 #pragma unroll
     for (int k = 0; k <= RT; ++k) h[k] = ht[k];
     const size_t st = (size_t)gridDim.x * 256;
-    for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
-        const size_t o = off0 + gi * V;
-        Raw raw[NW];
-#pragma unroll
-        for (int i = 0; i < NW; ++i) raw[i] = *reinterpret_cast<const Raw*>(reinterpret_cast<const T*>(fr.p[i]) + o);
-        auto val = [&](int i, int e) {
-            T t[V];
-            __builtin_memcpy(t, &raw[i], sizeof(Raw));
-            return (F)t[e];
-        };
-        F dt[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) dt[e] = val(RT, e) * h[0];
-#pragma unroll
-        for (int k = RT; k >= 1; --k)
-#pragma unroll
-            for (int e = 0; e < V; ++e) dt[e] = dt[e] + (val(RT - k, e) - val(RT + k, e)) * h[k];
-        if constexpr (sizeof(F) == 8) {
-            double2* d = reinterpret_cast<double2*>(D0 + gi * V);
-#pragma unroll
-            for (int i = 0; i < V / 2; ++i) d[i] = make_double2(dt[2 * i], dt[2 * i + 1]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < V; ++i) D0[gi * V + i] = dt[i];
-        }
-    }
+    for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st)
+        k0_group<T, F, RT>(fr, off0 + gi * V, h, D0 + gi * V);
 }
+
+// The NEXT frame's temporal derivative, computed inside the current frame's K5c (frame
+// pipelining, of3d_plan_execute_next): the K0 stage is pure HBM streaming and K5c is VALU-bound,
+// so its loads ride in K5c's memory slack instead of taking a launch of their own.
+template <typename F>
+struct K0Next {
+    Frames fr;        // frames c-rt .. c+rt of the next output frame
+    size_t off0;      // element offset of the first voxel (plane zb0) in each frame
+    size_t ngroups;   // vector groups of K0Vec<T>::V voxels
+    const F* ht;      // temporal taps h[0 .. rt]
+    F* D0;            // its dt0 (the plan's dt0 field, origin zb0)
+};
 
 // ---------------------------------------------------------------------------
 // K1: y and x passes of the gradient filters (calc_flow.py:279-288, y first):
@@ -2064,10 +2090,12 @@ __device__ __forceinline__ K5Block k5c_block() {
 // block holds ZC = 8 R output planes of 32 columns and its window of ZC + 2RW planes
 // per field takes NB buffers of HG 1-KiB row groups (fp64, RW 15: 24 KiB each).  Two
 // blocks fit a CU: one block's prologue / epilogue overlaps another's passes.
-template <typename F, typename RelT, int RW, int NB, int R, int NW = 4>
+// RT0 > 0: after its solve, every block also forms its share of the next frame's dt0 (K0Next,
+// input type T0): a contiguous range of voxel groups per block, the K0c arithmetic (k0_group).
+template <typename F, typename RelT, int RW, int NB, int R, int NW = 4, int RT0 = 0, typename T0 = uint16_t>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_solve_c(
     const F* __restrict__ Q, int zq0, int nz, int ny, int nx, size_t fs, const F* __restrict__ hw, int zo0, int nzo,
-    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel, int yo0) {
+    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel, int yo0, K0Next<F> k0) {
     // NW 8: 128-plane blocks (one per CU), window 1.33x the output planes instead of 1.66x
     constexpr int CB = 32, LPC = 64 / CB;  // columns per block, z-groups per wave
     constexpr int ZC = NW * LPC * R;                // output planes per block (R planes per z-group)
@@ -2106,6 +2134,26 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
     F acc[9][R];
 #pragma unroll
     for (int f = 0; f < NB - 1; ++f) issue(f, f);
+    // RT0 > 0: the next frame's dt0 for this block's first groups, loaded right behind the
+    // first field's DMA (the two latencies overlap) and held to the end (stores after the solve)
+    constexpr int V0 = K0Vec<T0>::V, NG0 = RT0 > 0 ? 2 : 0;
+    F dtn[NG0 > 0 ? NG0 : 1][V0];
+    size_t k0g0 = 0, k0g1 = 0;
+    if constexpr (RT0 > 0) {
+        const size_t nblk = (size_t)gridDim.x * gridDim.y * gridDim.z;
+        const size_t lin = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z);
+        const size_t per = (k0.ngroups + nblk - 1) / nblk;
+        k0g0 = lin * per;
+        k0g1 = min(k0g0 + per, k0.ngroups);
+        F h0[RT0 + 1];
+#pragma unroll
+        for (int k = 0; k <= RT0; ++k) h0[k] = k0.ht[k];
+#pragma unroll
+        for (int j = 0; j < NG0; ++j) {
+            const size_t gi = k0g0 + threadIdx.x + (size_t)j * 64 * NW;
+            if (gi < k0g1) k0_group_dt<T0, F, RT0>(k0.fr, k0.off0 + gi * V0, h0, dtn[j]);
+        }
+    }
 #pragma unroll
     for (int f = 0; f < 9; ++f) {
         // as k_wz_solve_dma: field f landed, the buffer the next issue overwrites is free
@@ -2123,9 +2171,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
 #pragma unroll
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
-    if (x >= nx) return;
-    k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
-                               vy, vz, rel);
+    if (x < nx)
+        k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
+                                   vy, vz, rel);
+    if constexpr (RT0 > 0) {  // the next frame's dt0: the held groups, then any rest of [k0g0, k0g1)
+#pragma unroll
+        for (int j = 0; j < NG0; ++j) {
+            const size_t gi = k0g0 + threadIdx.x + (size_t)j * 64 * NW;
+            if (gi < k0g1) k0_store<F, V0>(dtn[j], k0.D0 + gi * V0);
+        }
+        F h0[RT0 + 1];
+#pragma unroll
+        for (int k = 0; k <= RT0; ++k) h0[k] = k0.ht[k];
+        for (size_t gi = k0g0 + threadIdx.x + (size_t)NG0 * 64 * NW; gi < k0g1; gi += 64 * NW)
+            k0_group<T0, F, RT0>(k0.fr, k0.off0 + gi * V0, h0, k0.D0 + gi * V0);
+    }
 }
 // K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
 // float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each

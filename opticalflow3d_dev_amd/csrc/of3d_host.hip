@@ -45,12 +45,12 @@ enum : unsigned {
     KU_K0C = 1u << 0, KU_K0 = 1u << 1, KU_K1C = 1u << 2, KU_K1 = 1u << 3, KU_K12 = 1u << 4, KU_K2C = 1u << 5,
     KU_K2 = 1u << 6, KU_K34 = 1u << 7, KU_K34WS = 1u << 8, KU_K3 = 1u << 9, KU_K4 = 1u << 10, KU_K5C = 1u << 11,
     KU_K5C_PK = 1u << 12, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
-    KU_K34PK = 1u << 17,
+    KU_K34PK = 1u << 17, KU_K5C_NEXT = 1u << 18,
 };
 constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy_c",    "k_grad_xy",  "k_grad_xyz_c",
                                         "k_grad_z_c", "k_grad_z",     "k_prod_wyx",     "k_prod_wyx_ws", "k_prod_wy",
                                         "k_wx",       "k_wz_solve_c", "k_wz_solve_c2",  "k_wz_solve_dma", "k_wz_solve",
-                                        "k_solve2d",  "general",      "k_prod_wyx_pk"};
+                                        "k_solve2d",  "general",      "k_prod_wyx_pk",  "k_wz_solve_c_next"};
 
 struct of3d_plan {
     int ndim = 3;
@@ -79,6 +79,12 @@ struct of3d_plan {
     size_t k5c_lds = 0;
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
     bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
+    const void* k5c_next = nullptr;  // K5c that also forms the next frame's dt0 (frame pipelining)
+    // frame pipelining (of3d_plan_execute_next): the dt0 a previous call formed for these frames
+    bool pipe_valid = false;
+    const void* pipe_frames[kMaxT] = {};
+    int64_t pipe_fz0 = 0, pipe_zo0 = 0, pipe_zo1 = 0;
+    int pipe_dtype = 0;
     int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
     int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
     unsigned used = 0;       // kernel families launched so far (KU_* bits, of3d_plan_kernels)
@@ -319,6 +325,7 @@ int k34_setup(of3d_plan* p, int np) {
 template <typename F>
 int k5c_setup(of3d_plan* p) {
     p->k5c = nullptr;
+    p->k5c_next = nullptr;
     p->k5c_pk = false;
     p->k5c_nw = 4;
     if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
@@ -364,6 +371,15 @@ int k5c_setup(of3d_plan* p) {
     p->k5c_lds = nb * buf;
     OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
     p->k5c = fn;
+    // the same geometry with the next frame's K0 after the solve (uint16 frames; OF3D_PIPE=0: off)
+    p->k5c_next = nullptr;
+    if (const char* e = getenv("OF3D_PIPE"); !(e && e[0] == '0')) {
+        const void* fx = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r, nw, p->rt) : k5c_fn<F, float>(p->rw, nb, r, nw, p->rt);
+        if (fx) {
+            OF3D_HIP(hipFuncSetAttribute(fx, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
+            p->k5c_next = fx;
+        }
+    }
     return 0;
 }
 
@@ -655,7 +671,7 @@ int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, con
 // the results are those of the serial order (same kernels, same planes, global clamping).
 template <typename F>
 int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx_,
-          void* vy_, void* vz_, void* rel, hipStream_t s) {
+          void* vy_, void* vz_, void* rel, hipStream_t s, const void* const* d_next, bool pipe) {
     if (!p) return fail("of3d: null plan");
     F* vx = (F*)vx_;
     F* vy = (F*)vy_;
@@ -680,6 +696,29 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const size_t es = dtype_size(dtype);
     const int nwin = 2 * p->rt + 1;
     const int nf = d3 ? 9 : 5;
+    // frame pipelining: this call's dt0 was formed by the previous of3d_plan_execute_next call
+    // (inside its K5c) for exactly these frames and planes -> no K0 launch here
+    bool skip_k0 = pipe && p->pipe_valid && p->pipe_dtype == dtype && p->pipe_fz0 == frame_z0 &&
+                   p->pipe_zo0 == zo0 && p->pipe_zo1 == zo1;
+    for (int i = 0; skip_k0 && i < nwin; ++i) skip_k0 = p->pipe_frames[i] == d_frames[i];
+    p->pipe_valid = false;
+    // ... and this call's K5c forms the next frame's dt0 (serial schedule, uint16 frames, the
+    // vectorised K0 layout: every frame 8-byte aligned at plane zb0, whole groups of 4 voxels)
+    K0Next<F> k0n{};
+    bool fuse_next = false;
+    if (d_next && pipe && p->k5c_next && dtype == OF3D_U16 && !p->general && p->zchunk <= 0) {
+        const size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)(R.zb1 - R.zb0) * plane;
+        constexpr int V = K0Vec<uint16_t>::V;
+        fuse_next = off0 % V == 0 && n % V == 0;
+        for (int i = 0; fuse_next && i < nwin; ++i)
+            fuse_next = d_next[i] && ((uintptr_t)d_next[i] % (V * sizeof(uint16_t))) == 0;
+        if (fuse_next) {
+            for (int i = 0; i < nwin; ++i) k0n.fr.p[i] = d_next[i];
+            k0n.off0 = off0;
+            k0n.ngroups = n / V;
+            k0n.ht = tp.t;
+        }
+    }
     // K12 (fused gradient y/x/z passes, 3D): dt0 then lives in Y4 (K12 writes G = Y0..3
     // while other blocks still read dt0 planes), the pre-z fields B are never formed
     // (LDS-DMA staging: 16-byte rows and planes of dt0 and of the centre frame)
@@ -698,6 +737,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                           ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
     // field buffers
     F* D0b = k12 ? Y + 4 * fs : Y;     // temporal derivative (K0 -> K1 / K12), origin zb0
+    k0n.D0 = D0b;
     F* Bb = d3 ? Y + 4 * fs : X;       // pre-z fields (3D) / final gradients (2D), origin zb0
     const F* Gb = d3 ? Y : X;          // gradients, origin zg0
     F* Pb = d3 ? X : Y;                // K3 W-y (fallback) / K34 W-xy
@@ -707,43 +747,46 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     auto k01 = [&](int64_t b0, int64_t b1, hipStream_t st) -> int {
         if (b1 <= b0) return 0;
         const int nb = (int)(b1 - b0);
-        long long fstride = 0;
-        if (nwin > 1) {
-            const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
-            bool eq = d > 0 && d % (long long)es == 0;
-            for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
-            if (eq) fstride = d / (long long)es;
-        }
-        size_t off0 = (size_t)(b0 - frame_z0) * plane, n = (size_t)nb * plane;
-        int rt_arg = p->rt;
-        F* D0 = D0b + (size_t)(b0 - R.zb0) * plane;
-        const int V = k0_vec_width(dtype);
-        const size_t vb = (size_t)V * es;
-        bool vec = off0 % V == 0 && n % V == 0;
-        for (int i = 0; vec && i < nwin; ++i) vec = ((uintptr_t)d_frames[i] % vb) == 0;
-        if (vec) {
-            size_t ng = n / V;
-            const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
-            void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
-            const void* k0 = k0c_fn<F>(dtype, p->rt);
-            if (k0) {
-                void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
-                OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, st));
-                p->used |= KU_K0C;
+        if (!skip_k0) {  // (else: dt0 formed by the previous frame's K5c)
+            long long fstride = 0;
+            if (nwin > 1) {
+                const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
+                bool eq = d > 0 && d % (long long)es == 0;
+                for (int i = 2; eq && i < nwin; ++i) eq = ((const char*)d_frames[i] - (const char*)d_frames[i - 1]) == d;
+                if (eq) fstride = d / (long long)es;
+            }
+            size_t off0 = (size_t)(b0 - frame_z0) * plane, n = (size_t)nb * plane;
+            int rt_arg = p->rt;
+            F* D0 = D0b + (size_t)(b0 - R.zb0) * plane;
+            const int V = k0_vec_width(dtype);
+            const size_t vb = (size_t)V * es;
+            bool vec = off0 % V == 0 && n % V == 0;
+            for (int i = 0; vec && i < nwin; ++i) vec = ((uintptr_t)d_frames[i] % vb) == 0;
+            if (vec) {
+                size_t ng = n / V;
+                const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
+                void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
+                const void* k0 = k0c_fn<F>(dtype, p->rt);
+                if (k0) {
+                    void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
+                    OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, st));
+                    p->used |= KU_K0C;
+                } else {
+                    OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
+                    p->used |= KU_K0;
+                }
             } else {
-                OF3D_HIP(hipLaunchKernel(k0v_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
+                const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
+                void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
+                                (void*)&D0};
+                OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
                 p->used |= KU_K0;
             }
-        } else {
-            const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 256 * 16);
-            void* args[] = {(void*)&fr, (void*)&fstride, (void*)&off0, (void*)&n, (void*)&rt_arg, (void*)&tp.t,
-                            (void*)&D0};
-            OF3D_HIP(hipLaunchKernel(k0_kernel_dt<F>(dtype), dim3(blocks), dim3(256), args, 0, st));
-            p->used |= KU_K0;
         }
         if (k12) return 0;  // the y / x passes run inside K12 (stage grad_z)
-        const void* Ic = (const char*)d_frames[p->rt] + off0 * es;
-        const F* D0c = D0;
+        const size_t off1 = (size_t)(b0 - frame_z0) * plane;
+        const void* Ic = (const char*)d_frames[p->rt] + off1 * es;
+        const F* D0c = D0b + (size_t)(b0 - R.zb0) * plane;
         F* Bo = Bb + (size_t)(b0 - R.zb0) * plane;
         int need_b4 = d3, nb_arg = nb;
         dim3 g(cdiv(nx, 64 - 2 * p->rd), cdiv(ny, K1_TY), cdiv(nb, K1_NZB));
@@ -890,9 +933,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                 int yo0 = (int)p->ya;
                 void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny,  (void*)&nx,  (void*)&fs,
                                  (void*)&tp.w, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz,
-                                 (void*)&orel, (void*)&yo0};
-                OF3D_HIP(hipLaunchKernel(p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
-                p->used |= p->k5c_pk ? KU_K5C_PK : KU_K5C;
+                                 (void*)&orel, (void*)&yo0, (void*)&k0n};
+                OF3D_HIP(hipLaunchKernel(fuse_next ? p->k5c_next : p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
+                p->used |= fuse_next ? KU_K5C_NEXT : (p->k5c_pk ? KU_K5C_PK : KU_K5C);
             } else if (p->k5_nb) {
                 const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
                 OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5d_lds, st));
@@ -938,6 +981,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         nch = (int)std::min<int64_t>((nout + p->zchunk - 1) / p->zchunk, kMaxChunks);
         if (nch < 2) nch = 1;
     }
+    if (nch > 1) fuse_next = false;  // (zchunk > 0 already excluded it; kept as the invariant)
     if (nch == 1) {
         // serial: boundary i opens stage i and closes stage i-1; untimed stages get no events
         // (every event is a barrier packet between kernels: a few microseconds each)
@@ -956,6 +1000,14 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         if (!p->host_ev && p->timing_slots) {
             p->tchunks[slot] = 0;
             ++p->tcount;
+        }
+        if (fuse_next && p->k5c && d3) {  // the next call may skip its K0
+            p->pipe_valid = true;
+            for (int i = 0; i < nwin; ++i) p->pipe_frames[i] = d_next[i];
+            p->pipe_fz0 = frame_z0;
+            p->pipe_zo0 = zo0;
+            p->pipe_zo1 = zo1;
+            p->pipe_dtype = dtype;
         }
     } else {
         // overlap: chunk c = outputs [o_c, o_c+1); its G/Q planes end rw above, its B planes rd above that
@@ -995,10 +1047,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     return 0;
 }
 
+// pipe: an of3d_plan_execute_next call (may use the dt0 the previous such call formed for
+// these frames); d_next: the next output frame's frames (NULL: none)
 int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx,
-        void* vy, void* vz, void* rel, hipStream_t s) {
-    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s)
-                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
+        void* vy, void* vz, void* rel, hipStream_t s, const void* const* d_next = nullptr, bool pipe = false) {
+    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe)
+                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe);
 }
 
 void plan_free(of3d_plan* p);
@@ -1306,6 +1360,15 @@ int of3d_plan_execute(of3d_plan* p, const void* const* d_frames, int dtype, int6
     OF3D_HIP(hipSetDevice(p->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->stream;
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
+}
+
+int of3d_plan_execute_next(of3d_plan* p, const void* const* d_frames, const void* const* d_frames_next, int dtype,
+                           int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx, void* vy, void* vz, void* rel,
+                           void* stream) {
+    if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
+    OF3D_HIP(hipSetDevice(p->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_frames_next, true);
 }
 
 int of3d_plan_set_timing(of3d_plan* p, int slots) {

@@ -42,12 +42,14 @@ class FlowStream:
     """Device-resident sliding window over a frame sequence.
 
     push(frame) uploads one frame (shape vol_shape); once 2*rt+1 frames are
-    resident, submit() computes the flow of the window's centre frame and
-    returns a Pending whose .result() gives host arrays (vx, vy, [vz,] rel);
-    .release() hands the buffer set back (at most `depth` frames in flight)."""
+    resident, submit() computes the flow of the window's centre frame (the oldest
+    2*rt+1 resident frames; the oldest is then retired) and returns a Pending whose
+    .result() gives host arrays (vx, vy, [vz,] rel); .release() hands the buffer set
+    back (at most `depth` frames in flight).  With lookahead, push one frame more than
+    the window before submit() to pipeline the next window's temporal derivative."""
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
-                 d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None):
+                 d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None, lookahead=None):
         """zslab=(rank, world, group[, axis]): this process holds one slab of every frame (3D
         only) — axis 0 (default): output planes shard.zslab_bounds(nz, rank, world); axis 1:
         rows zslab_bounds(ny, rank, world) of every plane.  push() then takes the rank's own
@@ -57,7 +59,12 @@ class FlowStream:
         frame's compute; results are the rank's part of vx, vy, vz, rel (no gather).
         Row slabs run the plan on the rank's rows + halo as a volume of its own (the y pass is
         the first pass of both filter chains, so rows further than rd + rw from a cut are
-        exact: bit-identical), and keep the own rows."""
+        exact: bit-identical), and keep the own rows.
+
+        lookahead (default: on for whole-volume 3D streams): one more frame resident than the
+        window — push the next window's newest frame BEFORE submitting the current window, and
+        the current window's W-z/solve kernel also forms the next window's temporal derivative
+        (of3d_plan_execute_next, frame pipelining); the ring then has 2*rt+3 slots."""
         import torch
 
         from .shard import check_slab_split, halo_planes, zslab_bounds
@@ -79,6 +86,9 @@ class FlowStream:
         self.nz, self.ny, self.nx = nz, ny, nx
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.nwin = 2 * self.rt + 1
+        if lookahead is None:
+            lookahead = ndim == 3 and zslab is None
+        self.L = 1 if lookahead else 0
         if zslab is not None and ndim != 3:
             raise ValueError("z-slabs need a 3D volume")
         self.rank, self.world, self.group = zslab[:3] if zslab is not None else (0, 1, None)
@@ -123,11 +133,12 @@ class FlowStream:
                     self.rows_direct = True
                 except RuntimeError:  # kernels without row ranges: whole sub-volume, then a slice
                     pass
-        # nwin + 1 slots: a new frame's upload (and halo exchange) goes to the slot the
-        # frame before last read, so it overlaps the previous frame's compute
-        self.ring = torch.empty((self.nwin + 1, max(self.nblock, 1)), dtype=tdt, device=self.dev)
+        # nwin + 1 (+ lookahead) slots: a new frame's upload (and halo exchange) goes to the slot
+        # the frame before last read, so it overlaps the previous frame's compute
+        nslot = self.nwin + 1 + self.L
+        self.ring = torch.empty((nslot, max(self.nblock, 1)), dtype=tdt, device=self.dev)
         self.order = []  # ring slots of the resident frames, oldest first
-        self.free = list(range(self.nwin + 1))
+        self.free = list(range(nslot))
         self.dstage = torch.empty(max(self.nvox, 1), dtype=tdt, device=self.dev) if self.axis == 1 else None
         self.stage = [torch.empty(max(self.nvox, 1), dtype=tdt).pin_memory() for _ in range(2)]
         self.stage_np = [t.numpy().view(dt)[:self.nvox].reshape(self.shape) for t in self.stage]
@@ -184,9 +195,9 @@ class FlowStream:
         frame = np.asarray(frame)
         if frame.shape != self.shape:
             raise ValueError(f"frame shape {frame.shape} != stream shape {self.shape}")
-        if len(self.order) == self.nwin:  # recycle the oldest slot
-            self.free.append(self.order.pop(0))
-        slot = self.free.pop(0)
+        if not self.free:
+            raise RuntimeError("FlowStream: every ring slot holds a frame of an unsubmitted window")
+        slot = self.free.pop(0)  # the slot freed longest ago (its last reader is furthest done)
         st = self.stage[self.stage_i]
         if self.stage_evt[self.stage_i] is not None:
             self.stage_evt[self.stage_i].synchronize()  # pinned staging buffer free again
@@ -230,7 +241,11 @@ class FlowStream:
 
     @property
     def ready(self):
-        return len(self.order) == self.nwin
+        return len(self.order) >= self.nwin
+
+    @property
+    def lookahead(self):
+        return bool(self.L)
 
     def submit(self):
         torch = self.torch
@@ -241,11 +256,16 @@ class FlowStream:
         self.host_free[b].clear()  # which also means its D2H (and so its compute) finished
         dout, hout = self.dout[b], self.hout[b]
         self.comp.wait_stream(self.h2d)
-        ptrs = [self.ring[s].data_ptr() for s in self.order]
+        window = self.order[:self.nwin]
+        ptrs = [self.ring[s].data_ptr() for s in window]
+        # lookahead: the next window (one frame on) is resident too -> its dt0 formed in this call
+        nxt = [self.ring[s].data_ptr() for s in self.order[1:self.nwin + 1]] \
+            if self.L and len(self.order) == self.nwin + 1 else None
         vz = dout[2].data_ptr() if self.ndim == 3 else 0
         if self.plan is not None and self.axis == 0:
             self.plan.execute(ptrs, self.code, self.zi0, self.z0, self.z1 if self.ndim == 3 else 1,
-                              dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream)
+                              dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream,
+                              next_ptrs=nxt, pipelined=bool(self.L))
         elif self.plan is not None and self.rows_direct:  # row slab: the plan writes the own rows
             self.plan.execute(ptrs, self.code, 0, 0, self.nz, dout[0].data_ptr(), dout[1].data_ptr(),
                               dout[2].data_ptr(), dout[-1].data_ptr(), self.comp.cuda_stream)
@@ -258,8 +278,9 @@ class FlowStream:
                     d[:self.nvox].view(self.shape).copy_(self._rows(f)[:, self.y0 - self.yi0:self.y1 - self.yi0])
         cev = torch.cuda.Event()
         cev.record(self.comp)
-        for s in self.order:
+        for s in self.order[:self.nwin + self.L]:  # the window and (lookahead) the next frame
             self.slot_evt[s] = cev
+        self.free.append(self.order.pop(0))  # the window's oldest frame is done with (after cev)
         pending = Pending(self, b)
         if self.d2h_mode == "dma":
             self.dl_q.put((cev, hout, dout, pending))

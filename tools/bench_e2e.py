@@ -124,6 +124,8 @@ def main():
                     for k in fs.stats:
                         fs.stats[k] = 0
                     tr = fs.trace = [] if rep == 1 and os.environ.get("E2E_TRACE") else None
+                    fs.free += fs.order  # a fresh series (the previous rep's last frames retire)
+                    fs.order = []
                     for i in range(nt):
                         ta = time.perf_counter()
                         fs.push(mm[i])
@@ -131,7 +133,9 @@ def main():
                         if tr is not None:
                             tr += [(ta, f"push{i}"), (tb, "pushed")]
                         split["push"] += tb - ta
-                        if fs.ready:
+                        # lookahead: submit once the next window's newest frame is resident too
+                        # (frame pipelining); the last window goes without
+                        while len(fs.order) >= fs.nwin + fs.L or (i == nt - 1 and fs.ready):
                             pend.append(fs.submit())
                             tc = time.perf_counter()
                             split["submit"] += tc - tb
