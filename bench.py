@@ -135,6 +135,9 @@ def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane, sv=8):
         "prod_wy_wx": {"bytes": (4 * sv + 9 * sv) * ng * plane, "ops": (9 + 18 * C(rw)) * ng * plane},
         "wx": {"bytes": (9 * sv + 9 * sv) * ng * plane, "ops": 9 * C(rw) * ng * plane},
         "wz_solve": {"bytes": (9 * sv + 3 * sv + 4) * no * plane, "ops": (9 * C(rw) + 65 + 50) * no * plane},
+        # the next frame's temporal derivative (K0) when it runs inside the solve kernel
+        # (frame pipelining, k_wz_solve_c_next): its frames in, dt0 out
+        "tderiv_next": {"bytes": (nt_win * 2 + sv) * nb * plane, "ops": C(rt) * nb * plane},
     }
 
 
@@ -158,6 +161,17 @@ PLAN_FAMILIES = {"k_tderiv_c", "k_tderiv", "k_grad_xy_c", "k_grad_xy", "k_grad_x
                  "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk", "k_wz_solve_c_next"}
 
 
+def kernel_family(name):
+    """Plan family of a profiled kernel name: the solve kernel with a non-zero temporal radius
+    template argument (RT0, the 7th) carries the next frame's K0 (k_wz_solve_c_next)."""
+    base = name.split("<")[0]
+    if base == "k_wz_solve_c" and "<" in name:
+        args = [a.strip() for a in name.split("<", 1)[1].rstrip(">").split(",")]
+        if len(args) > 6 and args[6] != "0":
+            return "k_wz_solve_c_next"
+    return base
+
+
 def load_pmc_traffic(stage, cfg, used=None):
     """HBM bytes per launch of the stage's kernels from the committed rocprofv3 PMC summary
     (profiles/pmc_<cfg>.json: FETCH_SIZE x2 + WRITE_SIZE, calibrated in profiles/pmc_calibration.json).
@@ -176,13 +190,15 @@ def load_pmc_traffic(stage, cfg, used=None):
         for k, e in ks.items():
             for pre in STAGE_KERNELS[stage]:
                 if k.startswith(pre):
-                    base = k.split("<")[0]
+                    base = kernel_family(k)
                     if used and base in PLAN_FAMILIES and base not in used:
                         continue
                     rank = (e.get("dispatches", 0), -e.get("profiled_ms", 0.0))
                     if base not in best or rank > best[base][0]:
                         best[base] = (rank, e)
         best = {b: e for b, (_, e) in best.items()}
+        if used and "k_wz_solve_c_next" in used:
+            best.pop("k_wz_solve_c", None)  # the plain solve ran only on the series' first frame
         vals = [e.get("hbm_bytes_per_launch") for e in best.values()]
         if not vals or any(v is None for v in vals):
             return None
@@ -318,6 +334,9 @@ def roofline(profile, dom, dom_ms, model, cfg, frame_bytes, frame_ops, nwin, sv=
     B/voxel) over the frame's device time, the dominant kernel's PMC traffic, and the
     per-stage profile."""
     peak_v = FP64_VALU_PEAK_TOPS if sv == 8 else FP32_VALU_PEAK_TOPS
+    model = dict(model)
+    if dom == "wz_solve" and used and "k_wz_solve_c_next" in used:
+        model["wz_solve"] = {k: model["wz_solve"][k] + model["tderiv_next"][k] for k in ("bytes", "ops")}
     ach = model[dom]["ops"] / (dom_ms * 1e-3) / 1e12
     frame_ms = sum(profile.values())
     k_gbs = model[dom]["bytes"] / (dom_ms * 1e-3) / 1e9
