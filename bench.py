@@ -158,7 +158,8 @@ def fused_names(profile):
 # kernel families a plan reports (of3d_plan_kernels; kKernelNames in csrc/of3d_host.hip)
 PLAN_FAMILIES = {"k_tderiv_c", "k_tderiv", "k_grad_xy_c", "k_grad_xy", "k_grad_xyz_c", "k_grad_z_c", "k_grad_z",
                  "k_prod_wyx", "k_prod_wyx_ws", "k_prod_wy", "k_wx", "k_wz_solve_c", "k_wz_solve_c2",
-                 "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk", "k_wz_solve_c_next"}
+                 "k_wz_solve_dma", "k_wz_solve", "k_solve2d", "k_prod_wyx_pk", "k_wz_solve_c_next",
+                 "k_tderiv_multi"}
 
 
 def kernel_family(name):
@@ -368,7 +369,7 @@ class SlabBench:
     no exchange (the per-rank compute of the scaling model)."""
 
     def __init__(self, dims, sig, axis, rank, world, dev, fp32=False, timing=0, vrank=None, seed=20260206,
-                 pipeline=True):
+                 pipeline=True, k0_batch=0):
         import torch
 
         from opticalflow3d_dev_amd import _lib, make_taps, radii
@@ -403,9 +404,10 @@ class SlabBench:
                     self.plan.set_rows(self.a0 - self.ai0, self.a1 - self.ai0)
                 except RuntimeError:
                     self.rows_direct = False
-        # 2 rt + 2 slots (+ 1 with frame pipelining): the step's exchange goes to the slot the
-        # frame before last read
-        self.L = 1 if pipeline else 0
+        # 2 rt + 2 slots (+ 1 with frame pipelining, + M - 1 with K0 batching): the step's
+        # exchange goes to the slot the frame before last read
+        self.batch = min(k0_batch, 4) if k0_batch >= 2 else 0
+        self.L = self.batch - 1 if self.batch else (1 if pipeline else 0)
         nslot = self.nwin + 1 + self.L
         self.ring = torch.empty((nslot,) + self.blk_shape, dtype=torch.int16, device=dev)
         for f in range(nslot):
@@ -423,7 +425,7 @@ class SlabBench:
         self.xs = torch.cuda.Stream(device=dev)
         self.done = {}  # slot -> event of the last compute that read it
         self.xev = {}   # slot -> event of its frame's halo exchange (not yet waited for)
-        self.order = list(range(self.nwin + self.L))  # the window (+ the next window's newest frame)
+        self.order = list(range(self.nwin + self.L))  # the window (+ the lookahead frames)
 
     def _xchg_view(self, slot):
         v = self.ring[slot]
@@ -440,7 +442,9 @@ class SlabBench:
         rank's compute of the current window on the compute stream.  Without pipelining the
         new frame is the window's newest (the compute waits for its exchange); with it, the
         new frame is the NEXT window's newest (exchanged one step ahead, beside this compute)
-        and this compute forms the next window's dt0 (of3d_plan_execute_next)."""
+        and this compute forms the next window's dt0 (of3d_plan_execute_next); with K0
+        batching the M-1 frames after the window are resident and every M-th step's K0 forms
+        M windows' dt0 (of3d_plan_execute_ahead)."""
         import torch
 
         from opticalflow3d_dev_amd import _lib
@@ -463,14 +467,16 @@ class SlabBench:
         if compute:
             window = self.order[:self.nwin]
             ptrs = [self.ring[sl].data_ptr() for sl in window]
-            nxt = [self.ring[sl].data_ptr() for sl in self.order[1:]] if self.L else None
+            nxt = [self.ring[sl].data_ptr() for sl in self.order[1:]] if self.L and not self.batch else None
+            ahead = [self.ring[sl].data_ptr() for sl in self.order[self.nwin:]] if self.batch else None
+            pipe = bool(self.L) and not self.batch
             o = [t.data_ptr() for t in self.outs] + [self.rel.data_ptr()]
             if self.axis == 0:
                 self.plan.execute(ptrs, _lib.OF3D_U16, self.ai0, self.a0, self.a1, *o, self.comp.cuda_stream,
-                                  next_ptrs=nxt, pipelined=bool(self.L))
+                                  next_ptrs=nxt, pipelined=pipe, ahead_ptrs=ahead)
             else:
                 self.plan.execute(ptrs, _lib.OF3D_U16, 0, 0, self.dims[0], *o, self.comp.cuda_stream,
-                                  next_ptrs=nxt, pipelined=bool(self.L))
+                                  next_ptrs=nxt, pipelined=pipe, ahead_ptrs=ahead)
             ev = torch.cuda.Event()
             ev.record(self.comp)
             for sl in self.order:
@@ -514,14 +520,15 @@ def timed_steps(step, steps, warmup, world, dev):
     return max_over_ranks([el], dev)[0] if world > 1 else el
 
 
-def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=True):
+def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=True, k0_batch=0):
     """The default workload's frame split over the N ranks (strong scaling) — the path
     configs[3]/[4] and process_flow(parallel="zslab"/"yslab") run, on the headline volume:
     per-rank compute alone, the halo exchange alone (RCCL P2P of the newest frame's rd + rw
     planes / rows), and the pipelined step (exchange beside the previous step's compute).
     efficiency = the one-GPU frame time t1 (this run's replica step) / (N * step)."""
     nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
-    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50, pipeline=pipeline)
+    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50, pipeline=pipeline,
+                   k0_batch=k0_batch)
     try:
         comp = timed_steps(lambda: sb.step(exchange=False), steps, warmup, world, dev)
         xchg = timed_steps(lambda: sb.step(compute=False), steps, warmup, world, dev)
@@ -556,7 +563,8 @@ def run_slab(args, world, rank, local_rank, dev):
         axis = slab_axis(nz, ny, pworld, rd, rw)
     seed = 20260206 + (5 if fp32 else 4)
     sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32, timing=max(args.steps, 1),
-                   vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline)
+                   vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline,
+                   k0_batch=0 if args.no_pipeline else args.k0_batch)
     plan = sb.plan
     elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev)
     finite = sb.finite()
@@ -594,7 +602,10 @@ def run_slab(args, world, rank, local_rank, dev):
                        "parallelism": (f"virtual rank {prank} of {pworld} ({split}, compute only)" if vr else
                                        f"{split} x{world}, halo {rd + rw}" if world > 1 else "single GPU (whole frame)"),
                        "inputs": "own part of 2*rt+2 uint16 frames resident in HBM; per step the newest frame's "
-                                 "halo exchange (RCCL P2P, own stream) + compute", "outputs_finite": finite},
+                                 "halo exchange (RCCL P2P, own stream) + compute", "outputs_finite": finite,
+                       "series": (f"K0 batching: {sb.batch} windows per K0 pass (of3d_plan_execute_ahead), "
+                                  f"ring of {sb.nwin + 1 + sb.L} frames") if sb.batch else
+                                 ("frame pipelining (of3d_plan_execute_next)" if sb.L else "plain")},
             "roofline": roof, "cpu_baseline": cpu, "build": build_stamp(),
         }
         print(json.dumps(line), flush=True)
@@ -656,7 +667,12 @@ def main():
                     help="c4/c5: split axis of the volume over the ranks (auto: less halo work)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling split of the frame")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="no frame pipelining: every step launches its own K0 (of3d_plan_execute)")
+                    help="neither K0 batching nor frame pipelining: every step launches its own K0 "
+                         "(of3d_plan_execute)")
+    ap.add_argument("--k0-batch", type=int, default=int(os.environ.get("OF3D_BENCH_K0_BATCH", "4")),
+                    help="K0 batching (of3d_plan_execute_ahead, the default series mode): M = 2..4 consecutive "
+                         "windows of a series of 2rt+M resident frames, one K0 pass every M steps; 0 = frame "
+                         "pipelining (of3d_plan_execute_next) instead")
     ap.add_argument("--no-parity-sample", action="store_true", help="skip the oracle check of one output crop")
     ap.add_argument("--precision", default="fp64", choices=("fp64", "fp32"),
                     help="fp64 = bit-exact path (the metric's); fp32 = OF3D_FP32 (configs[4]'s path; c5 forces it)")
@@ -694,7 +710,10 @@ def main():
     nwin = 2 * rt + 1
     # the 2*rt+1 frames around the centre, generated on the device (synthetic_slab: the
     # SURVEY §8d family; every rank its own seed, i.e. its own output frame)
-    d_in = synthetic_slab(nwin, nz, ny, nx, 0, nz, 20260206 + int(args.config[1:]) + 100 * rank, dev)
+    kb = max(0, min(args.k0_batch, 4))
+    kb = kb if kb >= 2 and not args.no_pipeline else 0
+    nres = nwin + (kb - 1 if kb else 0)  # resident frames: the window (+ the batch's lookahead)
+    d_in = synthetic_slab(nres, nz, ny, nx, 0, nz, 20260206 + int(args.config[1:]) + 100 * rank, dev)
     vox = nz * ny * nx
     fp32 = args.precision == "fp32"
     sv = 4 if fp32 else 8
@@ -707,12 +726,24 @@ def main():
                      mode=_lib.OF3D_FP32 if fp32 else 0)
     if args.overlap >= 0:
         plan.set_overlap(args.overlap)
-    fptrs = [d_in[i].data_ptr() for i in range(nwin)]
+    aptrs = [d_in[i].data_ptr() for i in range(nres)]
+    fptrs = aptrs[:nwin]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    pipe = not args.no_pipeline
+    pipe = not args.no_pipeline and not kb
+    last = {"j": 0, "i": 0}
 
     def step():
+        if kb:
+            # K0 batching (of3d_plan_execute_ahead): step i is window j = i mod M of a series of
+            # 2rt+M resident frames; the j = 0 step forms the M windows' temporal derivatives in one
+            # pass, the next M-1 steps use theirs (every M timed steps run one batched K0)
+            j = last["i"] % kb
+            last["i"] += 1
+            last["j"] = j
+            plan.execute(aptrs[j:j + nwin], _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(),
+                         d_vz.data_ptr(), d_rel.data_ptr(), stream, ahead_ptrs=aptrs[j + nwin:])
+            return
         # frame pipelining (of3d_plan_execute_next): this step's W-z/solve kernel also forms the
         # next step's temporal derivative (the next frame of a series; here the same resident
         # frames), so every timed step runs K12 + K34 + K5c-with-the-next-K0
@@ -741,7 +772,7 @@ def main():
             if world > (nz, ny)[ax]:
                 continue
             r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step,
-                             pipeline=not args.no_pipeline)
+                             pipeline=not args.no_pipeline, k0_batch=kb)
             strong["zslab" if ax == 0 else "yslab"] = r
 
     if rank == 0:
@@ -752,14 +783,15 @@ def main():
         cpu = parity = None
         if world == 1 and not args.no_cpu_baseline:
             sub = min(cpu_sample_planes(nz, ny, nx, args.cpu_budget), nz)
-            host = d_in[:, :sub].cpu().numpy().view(np.uint16)
+            host = d_in[:nwin, :sub].cpu().numpy().view(np.uint16)
             cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
         if not args.no_parity_sample:
             # one 16^3 output crop across the kernels' seams (K5c / K12 z chunk 64, K34 row chunk
             # 256 at c3) against the oracle, outside the timed region
             zc, yc, xc = min(64, nz // 2), min(256, ny // 2), nx // 2 + 44
             box = (zc - 8, zc + 8, yc - 8, yc + 8, min(xc, nx - 16), min(xc, nx - 16) + 16)
-            parity = parity_sample(d_in, (d_vx, d_vy, d_vz, d_rel), box, s, t, w, fp32)
+            jl = last["j"]  # the window of the last step (its outputs are in d_v*)
+            parity = parity_sample(d_in[jl:jl + nwin], (d_vx, d_vy, d_vz, d_rel), box, s, t, w, fp32)
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
@@ -770,7 +802,11 @@ def main():
                        "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite,
                        "frame_pipelining": ("each step's W-z/solve kernel also forms the next step's temporal "
                                             "derivative (of3d_plan_execute_next); stage grad_xy is then empty")
-                       if pipe else None},
+                       if pipe else None,
+                       "k0_batch": (f"{kb} consecutive windows of a series of {nres} resident frames; one "
+                                    f"batched K0 pass (of3d_plan_execute_ahead) every {kb} steps"
+                                    + ("" if args.steps % kb == 0 else " (steps not a multiple: +-1 pass)"))
+                       if kb else None},
             "roofline": roof, "cpu_baseline": cpu,
             "parity_sample": parity, "build": build_stamp(),
         }

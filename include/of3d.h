@@ -163,6 +163,20 @@ int of3d_plan_execute_next(of3d_plan* plan, const void* const* d_frames, const v
                            int64_t frame_z0, int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz,
                            void* d_rel, void* stream);
 
+/* K0 batching for a time series (calc_flow.py:512-534 again): d_frames holds the frames
+ * c-rt .. c+rt+n_ahead (2*rt+1+n_ahead device pointers: the current window, then the next
+ * n_ahead frames, all resident and final when this call is enqueued).  of3d_plan_execute for
+ * the window d_frames[0 .. 2rt]; where the plan runs the fused gradient kernel (serial
+ * schedule, the vectorised frame layout) and no earlier call formed this window's temporal
+ * derivative, one pass over the 2rt+1+m frames forms it AND the next m-1 windows' (m =
+ * min(n_ahead, 3) + 1: 2rt+m frame reads for m derivatives instead of m(2rt+1)); the later
+ * of3d_plan_execute_ahead calls for exactly those windows (frame pointers, dtype, frame_z0,
+ * planes) skip their K0.  Calls on one stream (or otherwise ordered); any other execute call
+ * drops the formed derivatives.  Bit-identical to of3d_plan_execute. */
+int of3d_plan_execute_ahead(of3d_plan* plan, const void* const* d_frames, int n_ahead, int dtype, int64_t frame_z0,
+                            int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz, void* d_rel,
+                            void* stream);
+
 /* Per-stage timing with HIP events recorded on the launch stream.
  * of3d_plan_set_timing(plan, slots): keep a ring of `slots` executions
  * (0 = off; no host synchronisation is added to of3d_plan_execute).

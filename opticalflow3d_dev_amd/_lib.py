@@ -38,7 +38,7 @@ EXPORTED = (
     "of3d_plan_execute", "of3d_plan_stage_times", "of3d_stage_name", "of3d_plan_set_timing",
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
-    "of3d_plan_kernels", "of3d_build_info", "of3d_plan_execute_next",
+    "of3d_plan_kernels", "of3d_build_info", "of3d_plan_execute_next", "of3d_plan_execute_ahead",
 )
 
 CSRC = os.path.join(_HERE, "csrc")
@@ -169,6 +169,9 @@ def load():
         lib.of3d_plan_execute_next.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P), ctypes.c_int, i64, i64, i64,
                                                P, P, P, P, P]
         lib.of3d_plan_execute_next.restype = ctypes.c_int
+        lib.of3d_plan_execute_ahead.argtypes = [P, ctypes.POINTER(P), ctypes.c_int, ctypes.c_int, i64, i64, i64,
+                                                P, P, P, P, P]
+        lib.of3d_plan_execute_ahead.restype = ctypes.c_int
         lib.of3d_plan_stage_times.argtypes = [P, D, ctypes.c_int]
         lib.of3d_plan_stage_times.restype = ctypes.c_int
         lib.of3d_stage_name.argtypes = [ctypes.c_int]
@@ -267,9 +270,17 @@ class Plan:
         return a.value, b.value
 
     def execute(self, frame_ptrs, dtype_code, frame_z0, z_out0, z_out1, vx, vy, vz, rel, stream=0,
-                next_ptrs=None, pipelined=False):
+                next_ptrs=None, pipelined=False, ahead_ptrs=None):
         """of3d_plan_execute; pipelined=True: of3d_plan_execute_next (uses the dt0 the previous
-        pipelined call formed for these frames; with next_ptrs also forms the next frame's)."""
+        pipelined call formed for these frames; with next_ptrs also forms the next frame's);
+        ahead_ptrs (a list, possibly empty): of3d_plan_execute_ahead with the frames after the
+        window (K0 batching: one pass forms this and the next windows' dt0)."""
+        if ahead_ptrs is not None:
+            allp = list(frame_ptrs) + list(ahead_ptrs)
+            arr = (ctypes.c_void_p * len(allp))(*allp)
+            check(self.lib.of3d_plan_execute_ahead(self.handle, arr, len(ahead_ptrs), dtype_code, frame_z0, z_out0,
+                                                   z_out1, vx, vy, vz, rel, stream or None))
+            return
         arr = (ctypes.c_void_p * len(frame_ptrs))(*frame_ptrs)
         if not pipelined and next_ptrs is None:
             check(self.lib.of3d_plan_execute(self.handle, arr, dtype_code, frame_z0, z_out0, z_out1,

@@ -411,8 +411,8 @@ def _process_stream(load_frame, out_range, NtChunk, NtSlice, ndim, xyzSig, tSig,
         for hh in range(h0, h1):
             start = datetime.now()
             start_str = str(start)
-            # the window's frames, and (lookahead: frame pipelining) the next window's newest one
-            upto = hh + NtChunk + (1 if fs.lookahead and hh + 1 < h1 else 0)
+            # the window's frames, and (lookahead: frame pipelining / K0 batching) the next frames
+            upto = min(hh + NtChunk + fs.lookahead, h1 + NtChunk - 1)
             while pushed < upto:
                 fs.push(load_frame(pushed))
                 pushed += 1

@@ -8,6 +8,7 @@ template <typename F> const void* k1_kernel_dt(int dtype, int rd);          // k
 template <typename F> const void* k0v_kernel_dt(int dtype);                  // kt_grad_legacy.hip
 template <typename F> const void* k0_kernel_dt(int dtype);                   // kt_grad_legacy.hip
 template <typename F> const void* k0c_fn(int dtype, int rt);                 // kt_grad.hip
+template <typename F> const void* k0m_fn(int dtype, int rt, int m);          // kt_grad.hip (K0 batching)
 template <typename F> const void* k1c_fn(int dtype, int rd, int rs);         // kt_grad.hip
 template <typename F> const void* k12_fn(int dtype, int rd, int rs);         // kt_grad3.hip (fused y/x/z gradients)
 template <typename F> size_t k12_lds(int dtype, int rd);                     // kt_grad3.hip

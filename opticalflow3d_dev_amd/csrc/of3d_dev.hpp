@@ -332,6 +332,49 @@ __global__ __launch_bounds__(256) void k_tderiv_vec_c(Frames fr, size_t off0, si
         k0_group<T, F, RT>(fr, off0 + gi * V, h, D0 + gi * V);
 }
 
+// K0 batching (of3d_plan_execute_ahead): the temporal derivatives of M consecutive output
+// frames of a time series in one pass — frames c-rt .. c+M-1+rt, each loaded once (2rt + M
+// loads for M derivatives instead of M (2rt + 1)); output m (centre c + m) in the order of
+// k0_group_dt (bit-identical), to D0 + m * dstride.
+template <typename T, typename F, int RT, int M>
+__global__ __launch_bounds__(256) void k_tderiv_multi(Frames fr, size_t off0, size_t ngroups,
+                                                      const F* __restrict__ ht, F* __restrict__ D0,
+                                                      size_t dstride) {
+    constexpr int V = K0Vec<T>::V, NW = 2 * RT + M;
+    static_assert(NW <= kMaxT, "frame table");
+    using Raw = typename std::conditional<K0Vec<T>::B == 8, unsigned long long, uint4>::type;
+    F h[RT + 1];
+#pragma unroll
+    for (int k = 0; k <= RT; ++k) h[k] = ht[k];
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t gi = (size_t)blockIdx.x * 256 + threadIdx.x; gi < ngroups; gi += st) {
+        const size_t o = off0 + gi * V;
+        Raw raw[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) raw[i] = *reinterpret_cast<const Raw*>(reinterpret_cast<const T*>(fr.p[i]) + o);
+        auto val = [&](int i, int e) {
+            T t[V];
+            __builtin_memcpy(t, &raw[i], sizeof(Raw));
+            return (F)t[e];
+        };
+        F dt[M][V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) {  // one voxel at a time: its NW frame values converted once
+            F x[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) x[i] = val(i, e);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                dt[m][e] = x[RT + m] * h[0];
+#pragma unroll
+                for (int k = RT; k >= 1; --k) dt[m][e] = dt[m][e] + (x[RT + m - k] - x[RT + m + k]) * h[k];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) k0_store<F, V>(dt[m], D0 + m * dstride + gi * V);
+    }
+}
+
 // The NEXT frame's temporal derivative, computed inside the current frame's K5c (frame
 // pipelining, of3d_plan_execute_next): the K0 stage is pure HBM streaming and K5c is VALU-bound,
 // so its loads ride in K5c's memory slack instead of taking a launch of their own.

@@ -45,12 +45,13 @@ enum : unsigned {
     KU_K0C = 1u << 0, KU_K0 = 1u << 1, KU_K1C = 1u << 2, KU_K1 = 1u << 3, KU_K12 = 1u << 4, KU_K2C = 1u << 5,
     KU_K2 = 1u << 6, KU_K34 = 1u << 7, KU_K34WS = 1u << 8, KU_K3 = 1u << 9, KU_K4 = 1u << 10, KU_K5C = 1u << 11,
     KU_K5C_PK = 1u << 12, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
-    KU_K34PK = 1u << 17, KU_K5C_NEXT = 1u << 18,
+    KU_K34PK = 1u << 17, KU_K5C_NEXT = 1u << 18, KU_K0M = 1u << 19,
 };
 constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy_c",    "k_grad_xy",  "k_grad_xyz_c",
                                         "k_grad_z_c", "k_grad_z",     "k_prod_wyx",     "k_prod_wyx_ws", "k_prod_wy",
                                         "k_wx",       "k_wz_solve_c", "k_wz_solve_c2",  "k_wz_solve_dma", "k_wz_solve",
-                                        "k_solve2d",  "general",      "k_prod_wyx_pk",  "k_wz_solve_c_next"};
+                                        "k_solve2d",  "general",      "k_prod_wyx_pk",  "k_wz_solve_c_next",
+                                        "k_tderiv_multi"};
 
 struct of3d_plan {
     int ndim = 3;
@@ -85,6 +86,16 @@ struct of3d_plan {
     const void* pipe_frames[kMaxT] = {};
     int64_t pipe_fz0 = 0, pipe_zo0 = 0, pipe_zo1 = 0;
     int pipe_dtype = 0;
+    // K0 batching (of3d_plan_execute_ahead): dt0 slots Y4 .. Y4 + kDtSlots - 1 (K12 flow, whose
+    // workspace leaves Y4..Y8 free), each tagged with the window it was formed for; the call
+    // that uses a slot consumes it, and any other call drops them all
+    static constexpr int kDtSlots = 4;
+    struct DtSlot {
+        bool valid = false;
+        const void* frames[kMaxT] = {};
+        int dtype = 0;
+        int64_t fz0 = 0, zo0 = 0, zo1 = 0;
+    } dts[kDtSlots];
     int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
     int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
     unsigned used = 0;       // kernel families launched so far (KU_* bits, of3d_plan_kernels)
@@ -415,6 +426,21 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
 // K34 autotune at plan creation: every candidate geometry of k34_setup timed on the
 // plan's own workspace (whole volume, contents irrelevant to the time), the fastest kept.
 // Measured picks differ by config (c2: 2-wave blocks; c3: 4-wave blocks, 4-row tiles).
+// Tuning input: a deterministic pseudo-random field of gradient-like magnitudes.  Timings on
+// zeros run at a higher clock than on data (the fp64 VALU's DVFS give-back: c3 K34 1.41 ms
+// on zeros vs 1.64 on data) and need not rank the candidates as data does.
+template <typename F>
+__global__ __launch_bounds__(256) void k_fill_tune(F* __restrict__ p, size_t n) {
+    const size_t st = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += st) {
+        unsigned h = (unsigned)i * 2654435761u;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        p[i] = (F)((int)(h & 0xffffu) - 32768) * (F)(1.0 / 256);
+    }
+}
+
 template <typename F>
 int k34_tune(of3d_plan* p) {
     if (p->k34_cand.size() <= 1) return 0;
@@ -438,23 +464,31 @@ int k34_tune(of3d_plan* p) {
     for (size_t i = 0; i < p->k34_cand.size(); ++i)
         if (p->k34_cand[i].fn == p->k34.fn && p->k34_cand[i].cw == p->k34.cw && p->k34_cand[i].nthr == p->k34.nthr) h0 = i;
     std::swap(p->k34_cand[0], p->k34_cand[h0]);
-    float best = 1e30f;
-    size_t bi = 0;
-    for (size_t i = 0; i < p->k34_cand.size(); ++i) {
-        const auto& k = p->k34_cand[i];
-        OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));  // warm
-        float ms = 1e30f;
-        for (int rep = 0; rep < 2; ++rep) {  // best of two
+    const size_t nc = p->k34_cand.size();
+    // the gradient fields K34 reads (3D: 4, 2D: 3) as data-like values
+    const size_t nfill = (size_t)(p->ndim == 3 ? 4 : 3) * p->fs;
+    hipLaunchKernelGGL(k_fill_tune<F>, dim3(2048), dim3(256), 0, p->stream, G, nfill);
+    OF3D_HIP(hipGetLastError());
+    for (size_t i = 0; i < nc; ++i)  // warm every candidate (code load, caches)
+        OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+    // best of three, the candidates interleaved round-robin (clock drift over the tune hits
+    // every candidate alike)
+    std::vector<float> ms(nc, 1e30f);
+    for (int rep = 0; rep < 3; ++rep) {
+        for (size_t i = 0; i < nc; ++i) {
             OF3D_HIP(hipEventRecord(e0, p->stream));
-            OF3D_HIP(launch_k34(k, (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+            OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
             OF3D_HIP(hipEventRecord(e1, p->stream));
             OF3D_HIP(hipEventSynchronize(e1));
             float m = 0.f;
             OF3D_HIP(hipEventElapsedTime(&m, e0, e1));
-            ms = std::min(ms, m);
+            ms[i] = std::min(ms[i], m);
         }
-        if (i == 0 ? true : ms < 0.97f * best) best = ms, bi = i;
     }
+    float best = ms[0];
+    size_t bi = 0;
+    for (size_t i = 1; i < nc; ++i)
+        if (ms[i] < 0.97f * best) best = ms[i], bi = i;
     p->k34 = p->k34_cand[bi];
     if (getenv("OF3D_VERBOSE"))
         fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d thr=%d (%.3f ms)\n",
@@ -671,7 +705,7 @@ int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, con
 // the results are those of the serial order (same kernels, same planes, global clamping).
 template <typename F>
 int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx_,
-          void* vy_, void* vz_, void* rel, hipStream_t s, const void* const* d_next, bool pipe) {
+          void* vy_, void* vz_, void* rel, hipStream_t s, const void* const* d_next, bool pipe, int ahead) {
     if (!p) return fail("of3d: null plan");
     F* vx = (F*)vx_;
     F* vy = (F*)vy_;
@@ -735,8 +769,39 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     const void* k12 = (d3 && p->k12 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
                        ((k12_big && (sizeof(F) == 8 || p->rd <= 6)) || (k12_env && k12_env[0] == '1')))
                           ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
+    // K0 batching (of3d_plan_execute_ahead, `ahead` >= 0 frames past the window in d_frames):
+    // this call's dt0 from a slot an earlier call formed for exactly this window, else one
+    // k_tderiv_multi pass forms it and the next min(ahead, kDtSlots - 1) windows' (K12 flow,
+    // serial schedule, the vectorised K0 layout).  Same bits as K0 (k0_group_dt's order).
+    int dslot = 0, k0m = 0;  // slot holding this call's dt0; windows of a batched K0 launch
+    const void* k0m_k = nullptr;
+    Frames frm{};
+    if (ahead >= 0 && d3 && k12 && p->zchunk <= 0 && !p->general) {
+        for (int sl = 0; sl < of3d_plan::kDtSlots && !skip_k0; ++sl) {
+            auto& d = p->dts[sl];
+            bool hit = d.valid && d.dtype == dtype && d.fz0 == frame_z0 && d.zo0 == zo0 && d.zo1 == zo1;
+            for (int i = 0; hit && i < nwin; ++i) hit = d.frames[i] == d_frames[i];
+            if (hit) skip_k0 = true, dslot = sl, d.valid = false;  // consumed
+        }
+        const int m = std::min(ahead, of3d_plan::kDtSlots - 1) + 1;
+        if (!skip_k0)
+            for (auto& d : p->dts) d.valid = false;
+        if (!skip_k0 && m >= 2) {
+            const int V = k0_vec_width(dtype);
+            const size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)(R.zb1 - R.zb0) * plane;
+            bool vec = off0 % V == 0 && n % V == 0;
+            for (int i = 0; vec && i < nwin + m - 1; ++i) {
+                vec = d_frames[i] && ((uintptr_t)d_frames[i] % ((size_t)V * es)) == 0;
+                frm.p[i] = d_frames[i];
+            }
+            k0m_k = vec ? k0m_fn<F>(dtype, p->rt, m) : nullptr;
+            if (k0m_k) k0m = m;
+        }
+    } else {
+        for (auto& d : p->dts) d.valid = false;
+    }
     // field buffers
-    F* D0b = k12 ? Y + 4 * fs : Y;     // temporal derivative (K0 -> K1 / K12), origin zb0
+    F* D0b = k12 ? Y + (4 + dslot) * fs : Y;  // temporal derivative (K0 -> K1 / K12), origin zb0
     k0n.D0 = D0b;
     F* Bb = d3 ? Y + 4 * fs : X;       // pre-z fields (3D) / final gradients (2D), origin zb0
     const F* Gb = d3 ? Y : X;          // gradients, origin zg0
@@ -747,7 +812,15 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     auto k01 = [&](int64_t b0, int64_t b1, hipStream_t st) -> int {
         if (b1 <= b0) return 0;
         const int nb = (int)(b1 - b0);
-        if (!skip_k0) {  // (else: dt0 formed by the previous frame's K5c)
+        if (k0m) {  // batched K0: this window's dt0 (slot 0) and the next k0m - 1 windows'
+            size_t off0 = (size_t)(b0 - frame_z0) * plane, ng = (size_t)nb * plane / k0_vec_width(dtype);
+            F* D0 = Y + 4 * fs + (size_t)(b0 - R.zb0) * plane;
+            size_t dstride = fs;
+            const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
+            void* margs[] = {(void*)&frm, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0, (void*)&dstride};
+            OF3D_HIP(hipLaunchKernel(k0m_k, dim3(blocks), dim3(256), margs, 0, st));
+            p->used |= KU_K0M;
+        } else if (!skip_k0) {  // (else: dt0 formed by an earlier call: K5c's next / a batched K0)
             long long fstride = 0;
             if (nwin > 1) {
                 const long long d = (const char*)d_frames[1] - (const char*)d_frames[0];
@@ -981,7 +1054,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         nch = (int)std::min<int64_t>((nout + p->zchunk - 1) / p->zchunk, kMaxChunks);
         if (nch < 2) nch = 1;
     }
-    if (nch > 1) fuse_next = false;  // (zchunk > 0 already excluded it; kept as the invariant)
+    if (nch > 1) fuse_next = false, k0m = 0;  // (zchunk > 0 already excluded both; the invariant)
     if (nch == 1) {
         // serial: boundary i opens stage i and closes stage i-1; untimed stages get no events
         // (every event is a barrier packet between kernels: a few microseconds each)
@@ -1000,6 +1073,15 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         if (!p->host_ev && p->timing_slots) {
             p->tchunks[slot] = 0;
             ++p->tcount;
+        }
+        for (int j = 1; j < k0m; ++j) {  // the batched windows the next calls may skip K0 for
+            auto& d = p->dts[j];
+            d.valid = true;
+            for (int i = 0; i < nwin; ++i) d.frames[i] = d_frames[j + i];
+            d.dtype = dtype;
+            d.fz0 = frame_z0;
+            d.zo0 = zo0;
+            d.zo1 = zo1;
         }
         if (fuse_next && p->k5c && d3) {  // the next call may skip its K0
             p->pipe_valid = true;
@@ -1049,10 +1131,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
 
 // pipe: an of3d_plan_execute_next call (may use the dt0 the previous such call formed for
 // these frames); d_next: the next output frame's frames (NULL: none)
+// ahead >= 0: an of3d_plan_execute_ahead call (d_frames holds 2 rt + 1 + ahead frames)
 int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx,
-        void* vy, void* vz, void* rel, hipStream_t s, const void* const* d_next = nullptr, bool pipe = false) {
-    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe)
-                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe);
+        void* vy, void* vz, void* rel, hipStream_t s, const void* const* d_next = nullptr, bool pipe = false,
+        int ahead = -1) {
+    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead)
+                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead);
 }
 
 void plan_free(of3d_plan* p);
@@ -1369,6 +1453,15 @@ int of3d_plan_execute_next(of3d_plan* p, const void* const* d_frames, const void
     OF3D_HIP(hipSetDevice(p->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->stream;
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_frames_next, true);
+}
+
+int of3d_plan_execute_ahead(of3d_plan* p, const void* const* d_frames, int n_ahead, int dtype, int64_t frame_z0,
+                            int64_t zo0, int64_t zo1, void* vx, void* vy, void* vz, void* rel, void* stream) {
+    if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
+    if (n_ahead < 0 || 2 * p->rt + 1 + n_ahead > kMaxT) return fail("of3d: n_ahead out of range");
+    OF3D_HIP(hipSetDevice(p->device));
+    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, nullptr, false, n_ahead);
 }
 
 int of3d_plan_set_timing(of3d_plan* p, int slots) {

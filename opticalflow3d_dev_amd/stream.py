@@ -49,7 +49,7 @@ class FlowStream:
     the window before submit() to pipeline the next window's temporal derivative."""
 
     def __init__(self, ndim, vol_shape, dtype, xyzSig, tSig, wSig, device=None, depth=3, d2h="dma",
-                 d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None, lookahead=None):
+                 d2h_blocks=64, precision="fp64", rel_fp64=False, zslab=None, lookahead=None, k0_batch=None):
         """zslab=(rank, world, group[, axis]): this process holds one slab of every frame (3D
         only) — axis 0 (default): output planes shard.zslab_bounds(nz, rank, world); axis 1:
         rows zslab_bounds(ny, rank, world) of every plane.  push() then takes the rank's own
@@ -61,10 +61,13 @@ class FlowStream:
         the first pass of both filter chains, so rows further than rd + rw from a cut are
         exact: bit-identical), and keep the own rows.
 
-        lookahead (default: on for whole-volume 3D streams): one more frame resident than the
-        window — push the next window's newest frame BEFORE submitting the current window, and
-        the current window's W-z/solve kernel also forms the next window's temporal derivative
-        (of3d_plan_execute_next, frame pipelining); the ring then has 2*rt+3 slots."""
+        k0_batch=M (2..4; default 4 for whole-volume 3D streams unless `lookahead` is given):
+        M-1 frames of lookahead resident before submit (push them BEFORE submitting the current
+        window), and one K0 pass forms the temporal derivatives of M consecutive windows
+        (of3d_plan_execute_ahead: 2rt+M frame reads for M windows); the ring then has 2*rt+1+M
+        slots.  lookahead=True (with k0_batch unset or < 2): frame pipelining instead — one more
+        frame resident, and the current window's W-z/solve kernel forms the next window's
+        temporal derivative (of3d_plan_execute_next); 2*rt+3 slots.  Bit-identical either way."""
         import torch
 
         from .shard import check_slab_split, halo_planes, zslab_bounds
@@ -86,9 +89,15 @@ class FlowStream:
         self.nz, self.ny, self.nx = nz, ny, nx
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.nwin = 2 * self.rt + 1
+        self.batch = 0
+        if k0_batch is None:  # default: K0 batching of 4 windows for whole-volume 3D streams
+            k0_batch = 4 if lookahead is None else 0
+        if k0_batch >= 2 and ndim == 3 and zslab is None:
+            self.batch = min(int(k0_batch), 4)
+            lookahead = False
         if lookahead is None:
             lookahead = ndim == 3 and zslab is None
-        self.L = 1 if lookahead else 0
+        self.L = self.batch - 1 if self.batch else (1 if lookahead else 0)
         if zslab is not None and ndim != 3:
             raise ValueError("z-slabs need a 3D volume")
         self.rank, self.world, self.group = zslab[:3] if zslab is not None else (0, 1, None)
@@ -245,7 +254,8 @@ class FlowStream:
 
     @property
     def lookahead(self):
-        return bool(self.L)
+        """Frames past the window to push before submit (frame pipelining: 1; K0 batching: M-1)."""
+        return self.L
 
     def submit(self):
         torch = self.torch
@@ -260,12 +270,14 @@ class FlowStream:
         ptrs = [self.ring[s].data_ptr() for s in window]
         # lookahead: the next window (one frame on) is resident too -> its dt0 formed in this call
         nxt = [self.ring[s].data_ptr() for s in self.order[1:self.nwin + 1]] \
-            if self.L and len(self.order) == self.nwin + 1 else None
+            if self.L and not self.batch and len(self.order) == self.nwin + 1 else None
+        # K0 batching: the resident frames past the window (up to M-1; fewer at a series' end)
+        ahead = [self.ring[s].data_ptr() for s in self.order[self.nwin:self.nwin + self.L]] if self.batch else None
         vz = dout[2].data_ptr() if self.ndim == 3 else 0
         if self.plan is not None and self.axis == 0:
             self.plan.execute(ptrs, self.code, self.zi0, self.z0, self.z1 if self.ndim == 3 else 1,
                               dout[0].data_ptr(), dout[1].data_ptr(), vz, dout[-1].data_ptr(), self.comp.cuda_stream,
-                              next_ptrs=nxt, pipelined=bool(self.L))
+                              next_ptrs=nxt, pipelined=bool(self.L) and not self.batch, ahead_ptrs=ahead)
         elif self.plan is not None and self.rows_direct:  # row slab: the plan writes the own rows
             self.plan.execute(ptrs, self.code, 0, 0, self.nz, dout[0].data_ptr(), dout[1].data_ptr(),
                               dout[2].data_ptr(), dout[-1].data_ptr(), self.comp.cuda_stream)
