@@ -491,8 +491,12 @@ int k34_tune(of3d_plan* p) {
         if (ms[i] < 0.97f * best) best = ms[i], bi = i;
     p->k34 = p->k34_cand[bi];
     if (getenv("OF3D_VERBOSE"))
-        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cw=%d s=%d tx=%d nbx=%d thr=%d (%.3f ms)\n",
-                p->k34_cand.size(), p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, p->k34.nthr, best);
+        fprintf(stderr, "of3d: K34 tuned over %zu shapes: cand=%zu cw=%d s=%d tx=%d nbx=%d thr=%d lds=%zu (%.3f ms)\n",
+                p->k34_cand.size(), bi, p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, p->k34.nthr, p->k34.lds, best);
+    if (getenv("OF3D_VERBOSE") && atoi(getenv("OF3D_VERBOSE")) > 1)
+        for (size_t i = 0; i < nc; ++i)
+            fprintf(stderr, "of3d:   K34 cand %zu: cw=%d s=%d tx=%d thr=%d lds=%zu %.3f ms\n", i, p->k34_cand[i].cw,
+                    p->k34_cand[i].s, p->k34_cand[i].tx, p->k34_cand[i].nthr, p->k34_cand[i].lds, ms[i]);
     return 0;
 }
 
