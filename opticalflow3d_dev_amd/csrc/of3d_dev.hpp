@@ -998,8 +998,9 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // producers write tile t + 1 while consumers read tile t.  Same arithmetic and order as
 // k_prod_wyx (bit-identical).  128-VGPR budget (16 waves per CU): prefetch depth PD.
 // Ablation at c3 (round 2, timing-only experiment builds since removed): without the W-xy
-// stores 1.13 ms (the VALU ideal at the measured clock) vs 1.72; gradient loads from one
-// cache-resident row 1.48.  Staging the stores through a wave-private LDS transpose (whole
+// stores 1.13 ms vs 1.72 — but that build had no phase-B arithmetic either (dead code without
+// its stores; checked in the device assembly in round 3), i.e. the producers alone; gradient
+// loads from one cache-resident row 1.48.  Staging the stores through a wave-private LDS transpose (whole
 // rows per store instruction) measured slower (1.88 ms): the 72 B/voxel W-xy hand-off to
 // K5c itself, not its access pattern, is the cost.
 // (12-wave blocks — 4 consumer waves, 168 VGPRs, deeper prefetch, 8-row tiles — measured
