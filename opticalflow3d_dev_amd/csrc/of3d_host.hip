@@ -485,10 +485,12 @@ int k34_tune(of3d_plan* p) {
             ms[i] = std::min(ms[i], m);
         }
     }
-    float best = ms[0];
+    // the fastest candidate, unless it is within 3 % of the heuristic pick (index 0)
     size_t bi = 0;
     for (size_t i = 1; i < nc; ++i)
-        if (ms[i] < 0.97f * best) best = ms[i], bi = i;
+        if (ms[i] < ms[bi]) bi = i;
+    if (!(ms[bi] < 0.97f * ms[0])) bi = 0;
+    const float best = ms[bi];
     p->k34 = p->k34_cand[bi];
     if (getenv("OF3D_VERBOSE"))
         fprintf(stderr, "of3d: K34 tuned over %zu shapes: cand=%zu cw=%d s=%d tx=%d nbx=%d thr=%d lds=%zu (%.3f ms)\n",
