@@ -276,17 +276,21 @@ def max_over_ranks(values, dev):
     return [float(v) for v in t.cpu()]
 
 
-def timed_region(step, plan, args, world, dev):
+def timed_region(step, plan, args, world, dev, align=None):
     """warmup -> stage profile (K steps with all five stages timed, outside the timed
     region: every HIP event is a barrier packet between kernels, so timing all stages
     inflates the frame by ~8 %) -> the timed region: K steps bracketed by barrier +
     synchronize, with HIP events only around the dominant stage (the roofline kernel).
+    align: called (untimed) before the profile pass and the timed region — K0 batching puts
+    both on a batch boundary, so K steps hold ceil(K / M) batched K0 launches.
     Returns (elapsed_s, stage profile ms, dominant stage, its ms inside the timed region)."""
     import torch
     import torch.distributed as dist
 
     for _ in range(args.warmup):
         step()
+    if align:
+        align()
     torch.cuda.synchronize(dev)
     profile, dom, dom_ms = {}, None, None
     if plan is not None:
@@ -300,6 +304,8 @@ def timed_region(step, plan, args, world, dev):
         profile = fused_names(plan.stage_times())
         dom = max(profile, key=profile.get)
         plan.set_timing_stages(["prod_wy" if dom == "prod_wy_wx" else dom])
+    if align:
+        align()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -426,6 +432,7 @@ class SlabBench:
         self.done = {}  # slot -> event of the last compute that read it
         self.xev = {}   # slot -> event of its frame's halo exchange (not yet waited for)
         self.order = list(range(self.nwin + self.L))  # the window (+ the lookahead frames)
+        self.k = 0  # steps computed (K0 batching: step k % M == 0 forms M windows' dt0)
 
     def _xchg_view(self, slot):
         v = self.ring[slot]
@@ -481,6 +488,7 @@ class SlabBench:
             ev.record(self.comp)
             for sl in self.order:
                 self.done[sl] = ev
+            self.k += 1
         if self.L:
             self.order.pop(0)
             self.order.append(new)
@@ -566,7 +574,11 @@ def run_slab(args, world, rank, local_rank, dev):
                    vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline,
                    k0_batch=0 if args.no_pipeline else args.k0_batch)
     plan = sb.plan
-    elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev)
+    def align():
+        while sb.k % sb.batch:
+            sb.step()
+
+    elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev, align=align if sb.batch else None)
     finite = sb.finite()
     if world > 1:
         elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
@@ -750,7 +762,11 @@ def main():
         plan.execute(fptrs, _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(), d_vz.data_ptr(),
                      d_rel.data_ptr(), stream, next_ptrs=fptrs if pipe else None, pipelined=pipe)
 
-    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
+    def align():
+        while last["i"] % kb:
+            step()
+
+    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev, align=align if kb else None)
     if world > 1:
         (elapsed,) = max_over_ranks([elapsed], dev)
 
@@ -805,7 +821,9 @@ def main():
                        if pipe else None,
                        "k0_batch": (f"{kb} consecutive windows of a series of {nres} resident frames; one "
                                     f"batched K0 pass (of3d_plan_execute_ahead) every {kb} steps"
-                                    + ("" if args.steps % kb == 0 else " (steps not a multiple: +-1 pass)"))
+                                    + ("; the timed region starts on a batch" if args.steps % kb == 0 else
+                                       f"; the timed region starts on a batch: {-(-args.steps // kb)} passes in "
+                                       f"{args.steps} steps"))
                        if kb else None},
             "roofline": roof, "cpu_baseline": cpu,
             "parity_sample": parity, "build": build_stamp(),
