@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out; mkdir -p "$OUT"
 TAG=${TAG:-r03a}
-STAGES=${STAGES:-tests,smoke,bench,n2,prof}
+STAGES=${STAGES:-tests,smoke,bench,n2,cfgs,prof}
 has() { [[ ",$STAGES," == *",$1,"* ]]; }
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=10 --timeout 300 --timeout-method thread \
@@ -26,6 +26,12 @@ if has n2; then
   OF3D_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 > $OUT/bench_n2gloo_$TAG.log 2>&1 || exit $?
   tail -1 $OUT/bench_n2gloo_$TAG.log | cut -c1-300
+fi
+if has cfgs; then  # the other configs' bench lines (c2: configs[1]; c4: one GPU; c5: fp32, one GPU)
+  for cfg in ${BENCH_CFGS:-c2 c4 c5}; do
+    timeout -k 10 600 python bench.py --config $cfg --steps 12 --warmup 4 --no-cpu-baseline > $OUT/bench_${cfg}_$TAG.log 2>&1 || exit $?
+    tail -1 $OUT/bench_${cfg}_$TAG.log | cut -c1-200
+  done
 fi
 if has prof; then
   export TMPDIR=/tmp
