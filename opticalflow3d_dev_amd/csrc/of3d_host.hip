@@ -782,7 +782,8 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     int dslot = 0, k0m = 0;  // slot holding this call's dt0; windows of a batched K0 launch
     const void* k0m_k = nullptr;
     Frames frm{};
-    if (ahead >= 0 && d3 && k12 && p->zchunk <= 0 && !p->general) {
+    // (the fused W kernel writes W-xy to X; the K3 + K4 fallback writes it to Y over the slots)
+    if (ahead >= 0 && d3 && k12 && p->k34.fn && p->zchunk <= 0 && !p->general) {
         for (int sl = 0; sl < of3d_plan::kDtSlots && !skip_k0; ++sl) {
             auto& d = p->dts[sl];
             bool hit = d.valid && d.dtype == dtype && d.fz0 == frame_z0 && d.zo0 == zo0 && d.zo1 == zo1;

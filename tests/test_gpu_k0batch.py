@@ -71,6 +71,29 @@ def test_series_batched_equals_plain(sig, mode, m):
         ref.close()
 
 
+@pytest.mark.parametrize("env", [{"OF3D_K34": "0"}, {"OF3D_ZCHUNK": "8"}, {"OF3D_GENERAL": "1"}])
+def test_batching_off_paths(env, monkeypatch):
+    """Plans whose workspace or schedule cannot hold the batch (K3 + K4 instead of the fused W
+    kernel: W-xy lands on the slots; overlap chunks; the general-radius path) ignore the
+    lookahead and stay exact."""
+    import torch
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s, t, w = 2, 2, 5
+    nwin = 2 * radii(s, t, w)[2] + 1
+    stack, frames = _series(nwin + 4, s, t, w, 16)
+    plan = _lib.Plan(3, NZ, NY, NX, make_taps(s, t, w), device=0)
+    try:
+        for k in range(5):
+            got = _call(plan, frames, k, nwin, min(3, 4 - k), torch.float64, torch.float32)
+            for a, b in zip(got, calc_flow3D(stack[k:k + nwin], s, t, w)):
+                assert bits_equal(a, b), (env, k)
+        assert "k_tderiv_multi" not in plan.kernels(), plan.kernels()
+    finally:
+        plan.close()
+
+
 def test_out_of_order_and_plain_calls():
     """Batched windows used out of order, a plain call dropping the batch, a window whose
     frames are not the batch's (other pointers), the same window twice: all exact."""
@@ -140,3 +163,24 @@ def test_flowstream_k0_batch(m):
         assert "k_tderiv_multi" in fs.plan.kernels(), fs.plan.kernels()
     finally:
         fs.close()
+
+
+def test_process_flow_k0_batched(tmp_path, capsys):
+    """process_flow (calc_flow.py:362-625) through the batched K0: a OneTif series with 8
+    output frames, the driver pushing 3 frames of lookahead; every output TIFF equals the host
+    entry point's calc_flow3D of its window bit for bit (rel included)."""
+    from opticalflow3d_dev_amd import process_flow
+    from opticalflow3d_dev_amd import tiff as tf
+
+    s, t, w = 2, 1, 3
+    nwin = 2 * radii(s, t, w)[2] + 1
+    stack = np.random.default_rng(15).integers(0, 4096, size=(nwin + 7, NZ, NY, NX)).astype(np.uint16)
+    tf.imwrite(tmp_path / "b.tif", stack, imagej=True)
+    process_flow(str(tmp_path), "b", "OneTif", 3, s, t, w)
+    out = tmp_path / "OpticalFlow3D" / "b"
+    h = nwin // 2
+    for k in range(stack.shape[0] - nwin + 1):
+        got = [tf.imread(out / f"b_{n}_t{k + h:04d}.tiff") for n in ("vx", "vy", "vz", "rel")]
+        for a, b in zip(got, calc_flow3D(stack[k:k + nwin], s, t, w)):
+            assert bits_equal(a, b), k
+    assert capsys.readouterr().out.count("saved.  Duration") == stack.shape[0] - nwin + 1
