@@ -746,7 +746,8 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     // vectorised K0 layout: every frame 8-byte aligned at plane zb0, whole groups of 4 voxels)
     K0Next<F> k0n{};
     bool fuse_next = false;
-    if (d_next && pipe && p->k5c_next && dtype == OF3D_U16 && !p->general && p->zchunk <= 0) {
+    // (the fused W kernel keeps W-xy in X; with the K3 + K4 fallback K5c reads Y, where dt0 goes)
+    if (d_next && pipe && p->k5c_next && p->k34.fn && dtype == OF3D_U16 && !p->general && p->zchunk <= 0) {
         const size_t off0 = (size_t)(R.zb0 - frame_z0) * plane, n = (size_t)(R.zb1 - R.zb0) * plane;
         constexpr int V = K0Vec<uint16_t>::V;
         fuse_next = off0 % V == 0 && n % V == 0;

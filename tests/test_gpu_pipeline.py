@@ -78,6 +78,28 @@ def test_series_pipelined_equals_plain(sig, mode):
         plain_plan.close()
 
 
+@pytest.mark.parametrize("env", [{"OF3D_K34": "0"}, {"OF3D_K34": "0", "OF3D_K12": "1"}])
+def test_pipelining_off_with_k34_fallback(env, monkeypatch):
+    """Without the fused W kernel (K3 + K4: W-xy in Y, where the next dt0 would go) the plan
+    does not fuse the next frame's K0 into K5c, and the series stays exact."""
+    import torch
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s, t, w = 2, 2, 5
+    stack, wins, rt = _series((13 + 3, 16, 32, 40), s, t, w, 6)
+    plan = _lib.Plan(3, 16, 32, 40, make_taps(s, t, w), device=0)
+    try:
+        got = _run(plan, wins, None, (0, 16), (16, 32, 40), torch.float64,
+                   [(k, k + 1 if k + 1 < len(wins) else None, True) for k in range(len(wins))])
+        for k, g in enumerate(got):
+            for a, b in zip(g, calc_flow3D(stack[k:k + 2 * rt + 1], s, t, w)):
+                assert bits_equal(a, b), k
+        assert "k_wz_solve_c_next" not in plan.kernels(), plan.kernels()
+    finally:
+        plan.close()
+
+
 def test_break_in_series_recomputes():
     """execute_next(A, next=B) then a call for other frames (C): the pending dt0 (for B) must
     not be used; then B after C: recomputed too."""
