@@ -142,6 +142,7 @@ class FlowStream:
                     self.rows_direct = True
                 except RuntimeError:  # kernels without row ranges: whole sub-volume, then a slice
                     pass
+        depth = self._fit_device_memory(depth, tdt, ndim, precision, rel_fp64)
         # nwin + 1 (+ lookahead) slots: a new frame's upload (and halo exchange) goes to the slot
         # the frame before last read, so it overlaps the previous frame's compute
         nslot = self.nwin + 1 + self.L
@@ -198,6 +199,34 @@ class FlowStream:
             e.set()
         self.slot_evt = {}               # ring slot -> event of the last compute that read it
         self.k = 0
+
+    def _fit_device_memory(self, depth, tdt, ndim, precision, rel_fp64, margin=1 << 30):
+        """Output sets in flight and frames of lookahead that fit the device beside the plan's
+        workspace (already allocated): fewer output sets first, then K0 batching 4 -> 2 -> none
+        (frame pipelining: -> none); raises only when even one set and no lookahead do not fit.
+        Returns the depth; self.batch / self.L are updated."""
+        torch = self.torch
+        free = torch.cuda.mem_get_info(self.dev)[0] - margin
+        nout = 4 if ndim == 3 else 3
+        v_sz = 4 if precision == "fp32" else 8
+        rel_sz = 4 if precision == "fp32" else (8 if (ndim == 2 or rel_fp64) else 4)
+        set_b = max(self.nvox, 1) * ((nout - 1) * v_sz + rel_sz)
+        slot_b = max(self.nblock, 1) * torch.empty((), dtype=tdt).element_size()
+        fixed = slot_b * (self.nwin + 1) + (max(self.nvox, 1) * slot_b // max(self.nblock, 1) if self.axis == 1 else 0)
+        if self.axis == 1:  # row slabs without row ranges write a whole sub-volume set first
+            fixed += max(self.nblock, 1) * ((nout - 1) * v_sz + rel_sz)
+        need = lambda d, lk: fixed + lk * slot_b + d * set_b
+        while depth > 1 and need(depth, self.L) > free:
+            depth -= 1
+        while self.L and need(depth, self.L) > free:
+            if self.batch > 2:
+                self.batch, self.L = 2, 1
+            else:
+                self.batch, self.L = 0, 0
+        if need(depth, self.L) > free:
+            raise MemoryError(f"FlowStream: {need(depth, self.L) / 2**30:.1f} GiB of frames and outputs do not fit "
+                              f"the {free / 2**30:.1f} GiB left on device {self.device}")
+        return depth
 
     def push(self, frame):
         torch = self.torch

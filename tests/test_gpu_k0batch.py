@@ -184,3 +184,38 @@ def test_process_flow_k0_batched(tmp_path, capsys):
         for a, b in zip(got, calc_flow3D(stack[k:k + nwin], s, t, w)):
             assert bits_equal(a, b), k
     assert capsys.readouterr().out.count("saved.  Duration") == stack.shape[0] - nwin + 1
+
+
+@pytest.mark.parametrize("room,want", [(None, (3, 4, 3)), ("one_set_batch2", (1, 2, 1)), ("one_set_plain", (1, 0, 0))])
+def test_flowstream_fits_device_memory(room, want, monkeypatch):
+    """With little device memory left the stream keeps fewer output sets in flight, then less
+    lookahead (K0 batching 4 -> 2 -> none), and stays exact."""
+    import torch
+
+    from opticalflow3d_dev_amd.stream import FlowStream
+
+    s, t, w = 2, 2, 5
+    nwin = 13
+    vox = NZ * NY * NX
+    slot, oset = vox * 2, vox * (3 * 8 + 4)
+    if room is not None:
+        extra = {"one_set_batch2": 1, "one_set_plain": 0}[room]
+        fake = (1 << 30) + slot * (nwin + 1 + extra) + oset + 1024
+        real = torch.cuda.mem_get_info
+        monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (fake, real(dev)[1]))
+    stack = np.random.default_rng(17).integers(0, 3000, size=(nwin + 5, NZ, NY, NX)).astype(np.uint16)
+    fs = FlowStream(3, stack.shape[1:], np.uint16, s, t, w, depth=3)
+    try:
+        assert (fs.depth, fs.batch, fs.L) == want
+        k = 0
+        for i in range(stack.shape[0]):
+            fs.push(stack[i])
+            while len(fs.order) >= fs.nwin + fs.L or (i == stack.shape[0] - 1 and fs.ready):
+                p = fs.submit()
+                for a, b in zip(p.result(), calc_flow3D(stack[k:k + nwin], s, t, w)):
+                    assert bits_equal(a, b), k
+                p.release()
+                k += 1
+        assert k == stack.shape[0] - nwin + 1
+    finally:
+        fs.close()
