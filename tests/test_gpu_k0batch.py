@@ -219,3 +219,35 @@ def test_flowstream_fits_device_memory(room, want, monkeypatch):
         assert k == stack.shape[0] - nwin + 1
     finally:
         fs.close()
+
+
+@pytest.mark.parametrize("z0,z1", [(0, 14), (10, 24), (6, 18)])
+def test_zslab_subrange_batched(z0, z1):
+    """A z-slab plan (outputs [z0, z1), frames holding only the halo planes, frame_z0 = zi0) as
+    the slab bench runs it: a series through the batched K0 equals the same planes of the
+    whole-volume result."""
+    import torch
+
+    s, t, w = 2, 2, 5
+    rd, rs, rt, rw = radii(s, t, w)
+    nwin = 2 * rt + 1
+    stack = np.random.default_rng(18).integers(0, 4096, size=(nwin + 5, NZ, NY, NX)).astype(np.uint16)
+    zi0, zi1 = max(z0 - rd - rw, 0), min(z1 + rd + rw, NZ)
+    frames = [torch.from_numpy(np.ascontiguousarray(stack[i, zi0:zi1]).view(np.int16)).to("cuda")
+              for i in range(stack.shape[0])]
+    plan = _lib.Plan(3, NZ, NY, NX, make_taps(s, t, w), device=0, max_out_planes=z1 - z0)
+    try:
+        n = (z1 - z0) * NY * NX
+        for k in range(stack.shape[0] - nwin + 1):
+            outs = [torch.full((n,), float("nan"), dtype=torch.float64, device="cuda") for _ in range(3)]
+            outs.append(torch.full((n,), float("nan"), dtype=torch.float32, device="cuda"))
+            ptrs = [f.data_ptr() for f in frames[k:k + nwin]]
+            ahead = [f.data_ptr() for f in frames[k + nwin:k + nwin + 3]]
+            plan.execute(ptrs, _lib.OF3D_U16, zi0, z0, z1, *[o.data_ptr() for o in outs], ahead_ptrs=ahead)
+            torch.cuda.synchronize()
+            full = calc_flow3D(stack[k:k + nwin], s, t, w)
+            for a, b in zip(outs, full):
+                assert bits_equal(a.cpu().numpy().reshape(z1 - z0, NY, NX), b[z0:z1]), (k, z0, z1)
+        assert "k_tderiv_multi" in plan.kernels(), plan.kernels()
+    finally:
+        plan.close()
