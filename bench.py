@@ -787,8 +787,11 @@ def main():
         for ax in axes:
             if world > (nz, ny)[ax]:
                 continue
-            r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step,
-                             pipeline=not args.no_pipeline, k0_batch=kb)
+            try:  # the replica line stands on its own: a failed split is reported in it, not fatal
+                r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step,
+                                 pipeline=not args.no_pipeline, k0_batch=kb)
+            except Exception as e:  # noqa: BLE001
+                r = {"error": f"{type(e).__name__}: {e}"[:300]}
             strong["zslab" if ax == 0 else "yslab"] = r
 
     if rank == 0:
