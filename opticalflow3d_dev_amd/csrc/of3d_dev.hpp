@@ -1918,27 +1918,47 @@ __device__ __forceinline__ void solve3(double x2, double y2, double z2, double x
     vz = nR * ((xy * yz - y2 * xz) * tx + (xy * xz - x2 * yz) * ty + (x2 * y2 - xy * xy) * tz);
 }
 
-// cos(x) for x in [0, pi/3]: Taylor series to x^18 (truncation < 1e-18),
-// Horner with explicit FMAs (the eigen-solve is not bit-matched, see below).
-__device__ __forceinline__ double cos_small(double x) {
-    const double y = x * x;
-    double c = 1.0 / 6402373705728000.0;             // 1/18!
-    c = __builtin_fma(c, -y, 1.0 / 20922789888000.0);  // 1/16!
-    c = __builtin_fma(c, -y, 1.0 / 87178291200.0);     // 1/14!
-    c = __builtin_fma(c, -y, 1.0 / 479001600.0);       // 1/12!
-    c = __builtin_fma(c, -y, 1.0 / 3628800.0);         // 1/10!
-    c = __builtin_fma(c, -y, 1.0 / 40320.0);           // 1/8!
-    c = __builtin_fma(c, -y, 1.0 / 720.0);             // 1/6!
-    c = __builtin_fma(c, -y, 1.0 / 24.0);              // 1/4!
-    c = __builtin_fma(c, -y, 0.5);                     // 1/2!
-    return __builtin_fma(c, -y, 1.0);
+// cos((2/3) acos(u)) for u in [0, 1]: a degree-16 polynomial in t = 2u - 1 (Chebyshev fit,
+// monomial coefficients in t, |coef| <= 0.77: Horner is stable), max error 1.4e-15 — analytic on
+// [0, 1] (the acos branch points at u = +-1 cancel in the even cosine at u = 1; u = -1 is outside).
+// Coefficients from tools/eig_poly.py.  Replaces the library acos and a cos series (~110 VALU
+// instructions per voxel, a third of K5c's solve tail) by 16 FMAs.
+// one Horner step c * t + k with k in an SGPR pair (written out: the compiler's own choice, a
+// v_fmac_f64 with k moved into VGPRs first, costs two v_mov per coefficient and voxel)
+__device__ __forceinline__ double fma_sk(double c, double t, double k) {
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(c), "v"(t), "s"(k));
+    return d;
+}
+__device__ __forceinline__ double cos_two_thirds_acos(double u) {
+    const double t = 2.0 * u - 1.0;
+    double c = fma_sk(-1.627207239089953e-10, t, 5.267127096337474e-10);
+    c = fma_sk(c, t, -1.0560891259645176e-09);
+    c = fma_sk(c, t, 3.6015719568912613e-09);
+    c = fma_sk(c, t, -1.3476196916010413e-08);
+    c = fma_sk(c, t, 4.617990510403794e-08);
+    c = fma_sk(c, t, -1.594699400417876e-07);
+    c = fma_sk(c, t, 5.639770165191962e-07);
+    c = fma_sk(c, t, -2.035894233312921e-06);
+    c = fma_sk(c, t, 7.541131934033293e-06);
+    c = fma_sk(c, t, -2.8919931795498364e-05);
+    c = fma_sk(c, t, 0.00011642544430647587);
+    c = fma_sk(c, t, -0.0005041246915259092);
+    c = fma_sk(c, t, 0.0024663528157121257);
+    c = fma_sk(c, t, -0.015509188436476284);
+    c = fma_sk(c, t, 0.2474090663228402);
+    return fma_sk(c, t, 0.7660444431189779);
 }
 
 // Smallest eigenvalue of the symmetric 3x3 [[a d e][d b f][e f c]] in fp64
 // (trigonometric closed form).  The reference gets it from LAPACK cgeev in
 // complex64 (calc_flow.py:355-357); fp64 here, stored as float32 like the
 // reference's output (or kept fp64 with OF3D_REL_F64).
-// lambda_min = q + 2p cos(phi + 2pi/3) = q - 2p cos(pi/3 - phi), phi = acos(r)/3 in [0, pi/3].
+// lambda_min = q + 2p cos(phi + 2pi/3) = q - 2p cos(pi/3 - phi), phi = acos(r)/3 in [0, pi/3];
+// pi/3 - acos(r)/3 = (2/3) acos(u) with u = sqrt((1 - r) / 2) (acos(-r) = 2 acos(u)), so
+// lambda_min = q - 2p cos((2/3) acos(u)): one polynomial, no acos / cos.  Same conditioning as
+// the acos form (both see r near 1 through a square root): tools/eig_poly.py measures the two
+// forms equal against eigvalsh (max 1.4e-8 lambda_max, at near-degenerate pairs).
 __device__ __forceinline__ double eigmin3(double a, double b, double c, double d, double e, double f) {
     const double p1 = d * d + e * e + f * f;
     if (p1 == 0.0) return fmin(a, fmin(b, c));
@@ -1955,8 +1975,7 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
         B11 * (B22 * B33 - B23 * B23) - B12 * (B12 * B33 - B23 * B13) + B13 * (B12 * B23 - B22 * B13);
     double r = 0.5 * detB;
     r = fmin(1.0, fmax(-1.0, r));
-    const double phi = acos(r) * third;
-    return q - 2.0 * p * cos_small(1.0471975511965976 - phi);  // pi/3 - phi
+    return q - 2.0 * p * cos_two_thirds_acos(sqrt((1.0 - r) * 0.5));
 }
 
 // K5: W z pass + solve + reliability.  Block = 64 x-columns of one row and
