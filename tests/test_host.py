@@ -220,3 +220,43 @@ def test_percentile_threshold_matches_numpy(dtype):
             r = np.percentile(a, p)
             g = percentile_threshold(torch.from_numpy(a), p)
             assert r.dtype == g.dtype and r.tobytes() == np.asarray(g).tobytes(), (n, p)
+
+
+def test_eigenvalue_polynomial_pinned_to_its_generator():
+    """The device eigenvalue's cos((2/3) acos u) polynomial (csrc/of3d_dev.hpp,
+    cos_two_thirds_acos) carries exactly the coefficients tools/eig_poly.py fits, its error is
+    at fp64 rounding level, and the eigenvalue formula built on it matches the acos form it
+    replaced against eigvalsh (both limited by the r ~ 1 square-root conditioning)."""
+    import re
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import eig_poly
+
+    src = open(os.path.join(root, "opticalflow3d_dev_amd", "csrc", "of3d_dev.hpp")).read()
+    body = src[src.index("double cos_two_thirds_acos(double u)"):]
+    body = body[:body.index("\n}\n")]
+    lits = [float(x) for x in re.findall(r"fma_sk\((?:c|-?[0-9.e+-]+), t, (-?[0-9.e+-]+)\)", body)]
+    first = float(re.search(r"fma_sk\((-?[0-9.e+-]+), t,", body).group(1))
+    dev = [first] + lits  # highest degree first, as Horner runs
+    m = eig_poly.coefficients()
+    assert len(dev) == eig_poly.DEG + 1
+    # the generator's doubles, lowest degree first (a refit on another numpy / LAPACK may move
+    # the last bits, so not bit-for-bit)
+    assert np.allclose(np.array(dev[::-1]), m, rtol=1e-9, atol=1e-17)
+    u = np.linspace(0, 1, 100001)
+    assert np.abs(eig_poly.horner(m, 2 * u - 1) - np.cos(2 / 3 * np.arccos(u))).max() < 3e-15
+    rng = np.random.default_rng(3)
+    n = 20000
+    q, _ = np.linalg.qr(rng.standard_normal((n, 3, 3)))
+    lam = rng.standard_normal((n, 3))
+    lam[: n // 2, 1] = lam[: n // 2, 0] * (1 + 1e-9 * rng.standard_normal(n // 2))
+    a = np.einsum("nij,nj,nkj->nik", q, lam, q)
+    args = (a[:, 0, 0], a[:, 1, 1], a[:, 2, 2], a[:, 0, 1], a[:, 0, 2], a[:, 1, 2])
+    ref = np.linalg.eigvalsh(a)
+    lmax = np.abs(ref).max(axis=1)
+    err_poly = np.abs(eig_poly.eigmin3(*args, m=m) - ref[:, 0]) / lmax
+    err_acos = np.abs(eig_poly.eigmin3(*args) - ref[:, 0]) / lmax
+    assert err_poly.max() <= max(2 * err_acos.max(), 1e-12)
+    assert err_poly.max() < 1e-7
