@@ -1654,6 +1654,13 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 // Needs nx * sizeof(F) and nx * sizeof(T) multiples of 16 bytes and 16-byte aligned planes.
 // ---------------------------------------------------------------------------
 constexpr int K12_TY = 4;  // rows per block
+// z passes one step late (k_grad_xyz_c) in the fp32 kernels: c5 K12 18.2-18.5 -> 17.4 ms; the
+// fp64 kernel measured slower so (c3 0.602 -> 0.645 ms, same box, profiles/r03_ab/k12_defer/)
+#ifndef OF3D_K12_DEFER
+#define OF3D_K12_DEFER 1
+#endif
+template <typename F>
+constexpr bool k12_defer() { return OF3D_K12_DEFER && sizeof(F) == 4; }
 template <int RD>
 __host__ __device__ constexpr int k12_tx() { return 128 - 2 * RD; }
 // LDS bytes of one staged plane: NRW rows of dt0 (128 + EPL columns) and of I (128 + EPL_T)
@@ -1805,6 +1812,41 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
     //   step s:   [last step of a chunk: vmcnt(0) — retires the next chunk's DMA, issued a
     //             chunk ago] barrier [then: issue the chunk after it into the slots of the
     //             chunk just finished] x / z (s), y (s + 1)
+    // ---- z passes of step s (ring slot j = s mod NR): registers only ----
+    auto zpass = [&](int s, auto jc) {
+        constexpr int j = decltype(jc)::value;
+        auto slotz = [](int i, int n) { return ((i % n) + n) % n; };
+        if (s >= 2 * RD) {  // plane q = qa + s - 2 RD: dt and dz
+            const int q = qa + s - 2 * RD;
+            constexpr int cz = j - RD;
+            F o1 = r1[slotz(cz, NR)] * hg[0], o4 = r4[slotz(cz, NR)] * hd[0];
+#pragma unroll
+            for (int k = RD; k >= 1; --k) {
+                o1 = o1 + (r1[slotz(cz - k, NR)] + r1[slotz(cz + k, NR)]) * hg[k];
+                o4 = o4 + (r4[slotz(cz - k, NR)] - r4[slotz(cz + k, NR)]) * hd[k];
+            }
+            if (st_ok) {
+                const size_t pq = (size_t)(q - zg0) * plane;
+                buf_st<F>(o1, buf_rsrc(G + pq), vout, sout);
+                buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vout, sout);
+            }
+        }
+        if (s >= RD + RS && s < nout + RD + RS) {  // plane q = qa + s - RD - RS: dy and dx
+            const int q = qa + s - RD - RS;
+            constexpr int cz = j - RS;
+            F o2 = r2[slotz(cz, NRS)] * hs[0], o3 = r3[slotz(cz, NRS)] * hs[0];
+#pragma unroll
+            for (int k = RS; k >= 1; --k) {
+                o2 = o2 + (r2[slotz(cz - k, NRS)] + r2[slotz(cz + k, NRS)]) * hs[k];
+                o3 = o3 + (r3[slotz(cz - k, NRS)] + r3[slotz(cz + k, NRS)]) * hs[k];
+            }
+            if (st_ok) {
+                const size_t pq = (size_t)(q - zg0) * plane;
+                buf_st<F>(o2, buf_rsrc(G + fs + pq), vout, sout);
+                buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vout, sout);
+            }
+        }
+    };
     issue_chunk(0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     issue_chunk(1);
@@ -1824,6 +1866,11 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                         const int m2 = s / K + 2;
                         if (m2 * K < nsteps) issue_chunk(m2);
                     }
+                    // k12_defer: the z passes of step s - 1 here, ahead of this step's x-window
+                    // reads in program order: register-only work the scheduler can run while those
+                    // LDS reads are in flight (their ring slots exclude slot j, written below)
+                    if constexpr (k12_defer<F>())
+                        if (s >= 1) zpass(s - 1, std::integral_constant<int, (j + NR - 1) % NR>{});
                     // ---- x passes: thread (row `role`, staged column cx) of A tile s & 1 ----
                     // window [cx - R, cx + R] of a field row, as 16-byte pairs from the copy
                     // where it starts aligned
@@ -1861,38 +1908,8 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                     r3[j % NRS] = b3;
                     // ---- y passes of the next step (independent work for the scheduler) ----
                     if (s + 1 < nsteps) ypass_step(s + 1, (j + 1) & 1);
-                    // ---- z passes ----
-                    auto slotz = [](int i, int n) { return ((i % n) + n) % n; };
-                    if (s >= 2 * RD) {  // plane q = qa + s - 2 RD: dt and dz
-                        const int q = qa + s - 2 * RD;
-                        constexpr int cz = j - RD;
-                        F o1 = r1[slotz(cz, NR)] * hg[0], o4 = r4[slotz(cz, NR)] * hd[0];
-#pragma unroll
-                        for (int k = RD; k >= 1; --k) {
-                            o1 = o1 + (r1[slotz(cz - k, NR)] + r1[slotz(cz + k, NR)]) * hg[k];
-                            o4 = o4 + (r4[slotz(cz - k, NR)] - r4[slotz(cz + k, NR)]) * hd[k];
-                        }
-                        if (st_ok) {
-                            const size_t pq = (size_t)(q - zg0) * plane;
-                            buf_st<F>(o1, buf_rsrc(G + pq), vout, sout);
-                            buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vout, sout);
-                        }
-                    }
-                    if (s >= RD + RS && s < nout + RD + RS) {  // plane q = qa + s - RD - RS: dy and dx
-                        const int q = qa + s - RD - RS;
-                        constexpr int cz = j - RS;
-                        F o2 = r2[slotz(cz, NRS)] * hs[0], o3 = r3[slotz(cz, NRS)] * hs[0];
-#pragma unroll
-                        for (int k = RS; k >= 1; --k) {
-                            o2 = o2 + (r2[slotz(cz - k, NRS)] + r2[slotz(cz + k, NRS)]) * hs[k];
-                            o3 = o3 + (r3[slotz(cz - k, NRS)] + r3[slotz(cz + k, NRS)]) * hs[k];
-                        }
-                        if (st_ok) {
-                            const size_t pq = (size_t)(q - zg0) * plane;
-                            buf_st<F>(o2, buf_rsrc(G + fs + pq), vout, sout);
-                            buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vout, sout);
-                        }
-                    }
+                    // ---- z passes (k12_defer: at the next step; the last step's here) ----
+                    if (!k12_defer<F>() || s + 1 >= nsteps) zpass(s, std::integral_constant<int, j>{});
                     if (s + 1 >= nsteps) done = true;
                 }(),
                 ...);
