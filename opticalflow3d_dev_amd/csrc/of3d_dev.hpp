@@ -1985,14 +1985,31 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     const double q = (a + b + c) * third;
     const double aq = a - q, bq = b - q, cq = c - q;
     const double p2 = aq * aq + bq * bq + cq * cq + 2.0 * p1;
-    const double p = sqrt(p2 * sixth);
-    const double ip = 1.0 / p;
+    // p = sqrt(x) and 1 / p from one reciprocal square root (v_rsq_f64 + 2 Newton steps: ~1e-16
+    // relative; the IEEE sqrt and division sequences cost twice the instructions); tensors
+    // too small for the hardware estimate take the IEEE path (p1 > 0, so x > 0)
+    const double x = p2 * sixth;
+    double p, ip;
+    if (x > 1e-290 && x < 1e290) {
+        ip = __builtin_amdgcn_rsq(x);
+        ip = ip * (1.5 - 0.5 * x * ip * ip);
+        ip = ip * (1.5 - 0.5 * x * ip * ip);
+        p = x * ip;
+    } else {
+        p = sqrt(x);
+        ip = 1.0 / p;
+    }
     const double B11 = aq * ip, B22 = bq * ip, B33 = cq * ip, B12 = d * ip, B13 = e * ip, B23 = f * ip;
     const double detB =
         B11 * (B22 * B33 - B23 * B23) - B12 * (B12 * B33 - B23 * B13) + B13 * (B12 * B23 - B22 * B13);
     double r = 0.5 * detB;
     r = fmin(1.0, fmax(-1.0, r));
-    return q - 2.0 * p * cos_two_thirds_acos(sqrt((1.0 - r) * 0.5));
+    // u = sqrt(w), w in [0, 1], the same way (w floored at 1e-290: u < 1e-145 reads as 0)
+    const double w = fmax((1.0 - r) * 0.5, 1e-290);
+    double iu = __builtin_amdgcn_rsq(w);
+    iu = iu * (1.5 - 0.5 * w * iu * iu);
+    iu = iu * (1.5 - 0.5 * w * iu * iu);
+    return q - 2.0 * p * cos_two_thirds_acos(w * iu);
 }
 
 // K5: W z pass + solve + reliability.  Block = 64 x-columns of one row and
