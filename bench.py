@@ -412,7 +412,7 @@ class SlabBench:
                     self.rows_direct = False
         # 2 rt + 2 slots (+ 1 with frame pipelining, + M - 1 with K0 batching): the step's
         # exchange goes to the slot the frame before last read
-        self.batch = min(k0_batch, 4) if k0_batch >= 2 else 0
+        self.batch = min(k0_batch, 5) if k0_batch >= 2 else 0
         self.L = self.batch - 1 if self.batch else (1 if pipeline else 0)
         nslot = self.nwin + 1 + self.L
         self.ring = torch.empty((nslot,) + self.blk_shape, dtype=torch.int16, device=dev)
@@ -681,8 +681,8 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="neither K0 batching nor frame pipelining: every step launches its own K0 "
                          "(of3d_plan_execute)")
-    ap.add_argument("--k0-batch", type=int, default=int(os.environ.get("OF3D_BENCH_K0_BATCH", "4")),
-                    help="K0 batching (of3d_plan_execute_ahead, the default series mode): M = 2..4 consecutive "
+    ap.add_argument("--k0-batch", type=int, default=int(os.environ.get("OF3D_BENCH_K0_BATCH", "5")),
+                    help="K0 batching (of3d_plan_execute_ahead, the default series mode): M = 2..5 consecutive "
                          "windows of a series of 2rt+M resident frames, one K0 pass every M steps; 0 = frame "
                          "pipelining (of3d_plan_execute_next) instead")
     ap.add_argument("--no-parity-sample", action="store_true", help="skip the oracle check of one output crop")
@@ -722,7 +722,7 @@ def main():
     nwin = 2 * rt + 1
     # the 2*rt+1 frames around the centre, generated on the device (synthetic_slab: the
     # SURVEY §8d family; every rank its own seed, i.e. its own output frame)
-    kb = max(0, min(args.k0_batch, 4))
+    kb = max(0, min(args.k0_batch, 5))
     kb = kb if kb >= 2 and not args.no_pipeline else 0
     nres = nwin + (kb - 1 if kb else 0)  # resident frames: the window (+ the batch's lookahead)
     d_in = synthetic_slab(nres, nz, ny, nx, 0, nz, 20260206 + int(args.config[1:]) + 100 * rank, dev)

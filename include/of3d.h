@@ -169,7 +169,7 @@ int of3d_plan_execute_next(of3d_plan* plan, const void* const* d_frames, const v
  * the window d_frames[0 .. 2rt]; where the plan runs the fused gradient kernel (serial
  * schedule, the vectorised frame layout) and no earlier call formed this window's temporal
  * derivative, one pass over the 2rt+1+m frames forms it AND the next m-1 windows' (m =
- * min(n_ahead, 3) + 1: 2rt+m frame reads for m derivatives instead of m(2rt+1)); the later
+ * min(n_ahead, 4) + 1: 2rt+m frame reads for m derivatives instead of m(2rt+1)); the later
  * of3d_plan_execute_ahead calls for exactly those windows (frame pointers, dtype, frame_z0,
  * planes) skip their K0.  Calls on one stream (or otherwise ordered); any other execute call
  * drops the formed derivatives.  Bit-identical to of3d_plan_execute. */

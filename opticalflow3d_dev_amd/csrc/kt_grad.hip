@@ -22,13 +22,14 @@ const void* k0c_fn(int dtype, int rt) {
 #undef OF3D_K0C
 }
 
-// K0 batching instances (k_tderiv_multi): M = 2..4 consecutive outputs, the K0c dtypes and radii
+// K0 batching instances (k_tderiv_multi): M = 2..5 consecutive outputs, the K0c dtypes and radii
 template <typename F>
 const void* k0m_fn(int dtype, int rt, int m) {
 #define OF3D_K0M_M(T, RT)                                                    \
     if (m == 2) return (const void*)k_tderiv_multi<T, F, RT, 2>;            \
     if (m == 3) return (const void*)k_tderiv_multi<T, F, RT, 3>;            \
     if (m == 4) return (const void*)k_tderiv_multi<T, F, RT, 4>;            \
+    if (m == 5) return (const void*)k_tderiv_multi<T, F, RT, 5>;            \
     return nullptr;
 #define OF3D_K0M(T)                         \
     if (rt == 3) { OF3D_K0M_M(T, 3) }       \

@@ -89,7 +89,7 @@ struct of3d_plan {
     // K0 batching (of3d_plan_execute_ahead): dt0 slots Y4 .. Y4 + kDtSlots - 1 (K12 flow, whose
     // workspace leaves Y4..Y8 free), each tagged with the window it was formed for; the call
     // that uses a slot consumes it, and any other call drops them all
-    static constexpr int kDtSlots = 4;
+    static constexpr int kDtSlots = 5;  // Y4 .. Y8
     struct DtSlot {
         bool valid = false;
         const void* frames[kMaxT] = {};

@@ -61,7 +61,7 @@ class FlowStream:
         the first pass of both filter chains, so rows further than rd + rw from a cut are
         exact: bit-identical), and keep the own rows.
 
-        k0_batch=M (2..4; default 4 for whole-volume 3D streams unless `lookahead` is given):
+        k0_batch=M (2..5; default 5 for whole-volume 3D streams unless `lookahead` is given):
         M-1 frames of lookahead resident before submit (push them BEFORE submitting the current
         window), and one K0 pass forms the temporal derivatives of M consecutive windows
         (of3d_plan_execute_ahead: 2rt+M frame reads for M windows); the ring then has 2*rt+1+M
@@ -90,10 +90,10 @@ class FlowStream:
         self.rd, self.rs, self.rt, self.rw = radii(xyzSig, tSig, wSig)
         self.nwin = 2 * self.rt + 1
         self.batch = 0
-        if k0_batch is None:  # default: K0 batching of 4 windows for whole-volume 3D streams
-            k0_batch = 4 if lookahead is None else 0
+        if k0_batch is None:  # default: K0 batching of 5 windows for whole-volume 3D streams
+            k0_batch = 5 if lookahead is None else 0
         if k0_batch >= 2 and ndim == 3 and zslab is None:
-            self.batch = min(int(k0_batch), 4)
+            self.batch = min(int(k0_batch), 5)
             lookahead = False
         if lookahead is None:
             lookahead = ndim == 3 and zslab is None
@@ -202,7 +202,7 @@ class FlowStream:
 
     def _fit_device_memory(self, depth, tdt, ndim, precision, rel_fp64, margin=1 << 30):
         """Output sets in flight and frames of lookahead that fit the device beside the plan's
-        workspace (already allocated): fewer output sets first, then K0 batching 4 -> 2 -> none
+        workspace (already allocated): fewer output sets first, then K0 batching M -> 2 -> none
         (frame pipelining: -> none); raises only when even one set and no lookahead do not fit.
         Returns the depth; self.batch / self.L are updated."""
         torch = self.torch

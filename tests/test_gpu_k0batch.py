@@ -43,7 +43,8 @@ def _call(plan, frames, k, nwin, n_ahead, vt, reld, plain=False):
     return [o.cpu().numpy().reshape(NZ, NY, NX) for o in outs]
 
 
-@pytest.mark.parametrize("sig,mode,m", [((2, 2, 5), 0, 4), ((2, 3, 7), 0, 4), ((2, 3, 7), 0, 2),
+@pytest.mark.parametrize("sig,mode,m", [((2, 2, 5), 0, 4), ((2, 3, 7), 0, 4), ((2, 3, 7), 0, 2), ((2, 3, 7), 0, 5),
+                                        ((2, 2, 5), _lib.OF3D_FP32, 5),
                                         ((2, 2, 5), _lib.OF3D_FP32, 4), ((2, 3, 7), _lib.OF3D_REL_F64, 3)])
 def test_series_batched_equals_plain(sig, mode, m):
     import torch
@@ -133,7 +134,7 @@ def test_copied_window_not_matched():
         plan.close()
 
 
-@pytest.mark.parametrize("m", [2, 4])
+@pytest.mark.parametrize("m", [2, 4, 5])
 def test_flowstream_k0_batch(m):
     """The streaming driver with K0 batching: every output equals calc_flow3D of its window."""
     from opticalflow3d_dev_amd.stream import FlowStream
@@ -186,10 +187,10 @@ def test_process_flow_k0_batched(tmp_path, capsys):
     assert capsys.readouterr().out.count("saved.  Duration") == stack.shape[0] - nwin + 1
 
 
-@pytest.mark.parametrize("room,want", [(None, (3, 4, 3)), ("one_set_batch2", (1, 2, 1)), ("one_set_plain", (1, 0, 0))])
+@pytest.mark.parametrize("room,want", [(None, (3, 5, 4)), ("one_set_batch2", (1, 2, 1)), ("one_set_plain", (1, 0, 0))])
 def test_flowstream_fits_device_memory(room, want, monkeypatch):
     """With little device memory left the stream keeps fewer output sets in flight, then less
-    lookahead (K0 batching 4 -> 2 -> none), and stays exact."""
+    lookahead (K0 batching 5 -> 2 -> none), and stays exact."""
     import torch
 
     from opticalflow3d_dev_amd.stream import FlowStream
