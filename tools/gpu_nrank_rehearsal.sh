@@ -9,9 +9,9 @@ OUT=gpurun_out; mkdir -p $OUT
 export OF3D_BENCH_BACKEND=gloo
 for n in ${NS:-4 6}; do
   timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $((29540 + n)) bench.py --gpus $n --steps 5 --warmup 2 > $OUT/bench_n${n}_gloo_r03h.log 2>&1 \
-    || { tail -20 $OUT/bench_n${n}_gloo_r03h.log; exit 1; }
-  grep '^{"metric"' $OUT/bench_n${n}_gloo_r03h.log | python3 -c "
+    --master-port $((29540 + n)) bench.py --gpus $n --steps 5 --warmup 2 > $OUT/bench_n${n}_gloo_${TAG:-r03i}.log 2>&1 \
+    || { tail -20 $OUT/bench_n${n}_gloo_${TAG:-r03i}.log; exit 1; }
+  grep '^{"metric"' $OUT/bench_n${n}_gloo_${TAG:-r03i}.log | python3 -c "
 import json,sys
 d=json.loads(sys.stdin.read())
 print('N=%d value %.1f ms/step %.3f' % (d['n_gpus'], d['value'], d['ms_per_step']))
