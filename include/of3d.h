@@ -239,6 +239,15 @@ int of3d_flow_stats(const void* vx, const void* vy, const void* vz, const void* 
                     int64_t n, double thresh, double xyscale, double zscale, double tscale, double* out_vx,
                     double* out_vy, double* out_vz, double* magnitude, double* theta, double* phi, void* stream);
 
+/* Reliability (smallest eigenvalue) of n given symmetric 3x3 structure tensors
+ * resident on the device: `tensor` is field-major [6][n] float64 in the order
+ * x2 y2 z2 xy xz yz (calc_flow.py:352-354's matrix (x2 xy xz / xy y2 yz /
+ * xz yz z2)); `rel` receives float32 (the reference's complex64 cgeev
+ * precision, calc_flow.py:355-357) or, with rel_f64, float64 (MATLAB's double
+ * pageeig, M/calc_flow3D.m:235-236) — exactly the values the flow kernels
+ * store for those tensors.  Enqueued on `stream`. */
+int of3d_rel3d(const double* tensor, int64_t n, void* rel, int rel_f64, void* stream);
+
 /* Blocking copy of n buffers on the GPU's DMA (SDMA) engines through the HSA
  * runtime: no compute units and no HIP stream involved, so a download does
  * not contend with kernels for the memory pipeline.  Host buffers must be

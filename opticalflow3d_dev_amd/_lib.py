@@ -39,6 +39,7 @@ EXPORTED = (
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
     "of3d_plan_kernels", "of3d_build_info", "of3d_plan_execute_next", "of3d_plan_execute_ahead",
+    "of3d_rel3d",
 )
 
 CSRC = os.path.join(_HERE, "csrc")
@@ -189,6 +190,8 @@ def load():
         d = ctypes.c_double
         lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
         lib.of3d_flow_stats.restype = ctypes.c_int
+        lib.of3d_rel3d.argtypes = [P, i64, P, ctypes.c_int, P]
+        lib.of3d_rel3d.restype = ctypes.c_int
         lib.of3d_copy_async.argtypes = [P, P, ctypes.c_size_t, ctypes.c_int, P]
         lib.of3d_copy_async.restype = ctypes.c_int
         lib.of3d_dma_copy.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),

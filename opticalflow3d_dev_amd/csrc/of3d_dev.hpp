@@ -1974,8 +1974,56 @@ __device__ __forceinline__ double cos_two_thirds_acos(double u) {
 // lambda_min = q + 2p cos(phi + 2pi/3) = q - 2p cos(pi/3 - phi), phi = acos(r)/3 in [0, pi/3];
 // pi/3 - acos(r)/3 = (2/3) acos(u) with u = sqrt((1 - r) / 2) (acos(-r) = 2 acos(u)), so
 // lambda_min = q - 2p cos((2/3) acos(u)): one polynomial, no acos / cos.  Same conditioning as
-// the acos form (both see r near 1 through a square root): tools/eig_poly.py measures the two
-// forms equal against eigvalsh (max 1.4e-8 lambda_max, at near-degenerate pairs).
+// the acos form: near r = 1 (the two SMALLEST eigenvalues nearly equal: flat / isotropic or
+// rank-1 regions) r's rounding reaches u through a square root, an error of ~sqrt(eps) p —
+// tools/eig_poly.py measures 1.7e-8 lambda_max there.  That is far inside the float32 rel's
+// 1e-6 lambda_max, but not the fp64 rel's 1e-10 (OF3D_REL_F64, MATLAB's pageeig,
+// M/calc_flow3D.m:235-236), so the fp64-rel instances (REFINE) take eigmin3_deflate below for
+// w = (1 - r) / 2 < 1e-6: there lambda_max is simple and far from the pair, so its eigenvector
+// is well conditioned, and the pair's smaller eigenvalue comes from the 2x2 block on the plane
+// orthogonal to it with the cancellation-free 2x2 formula (max 1e-13 lambda_max over
+// tools/eig_poly.py's near-degenerate, isotropic and rank-1 sets; tests/test_eig_formula.py).
+// The branch is taken by whole waves only where such tensors occur; float32-rel instances
+// never compile it.
+__device__ __forceinline__ double eigmin3_deflate(double aq, double bq, double cq, double d, double e, double f,
+                                               double p, double w) {
+    // E = T - qI (entries aq bq cq / d e f); its largest eigenvalue 2p cos(phi) with
+    // phi = (2/3) asin(u): cos(phi) = 1 - (2/9) w + O(w^2) (an error in mu only tilts the
+    // eigenvector, which moves the 2x2 block's eigenvalues at second order)
+    const double mu = 2.0 * p * (1.0 - (2.0 / 9.0) * w);
+    const double m00 = aq - mu, m11 = bq - mu, m22 = cq - mu;
+    // the eigenvector of mu: the longest cross product of two rows of E - mu I (rank 2)
+    const double c0x = d * f - e * m11, c0y = e * d - m00 * f, c0z = m00 * m11 - d * d;
+    const double c1x = d * m22 - e * f, c1y = e * e - m00 * m22, c1z = m00 * f - d * e;
+    const double c2x = m11 * m22 - f * f, c2y = f * e - d * m22, c2z = d * f - m11 * e;
+    const double n0 = c0x * c0x + c0y * c0y + c0z * c0z, n1 = c1x * c1x + c1y * c1y + c1z * c1z,
+                 n2 = c2x * c2x + c2y * c2y + c2z * c2z;
+    double vx = c0x, vy = c0y, vz = c0z, nn = n0;
+    if (n1 > nn) vx = c1x, vy = c1y, vz = c1z, nn = n1;
+    if (n2 > nn) vx = c2x, vy = c2y, vz = c2z, nn = n2;
+    const double iv = 1.0 / sqrt(nn);
+    vx *= iv, vy *= iv, vz *= iv;
+    // an orthonormal basis (u1, u2) of the plane orthogonal to v
+    double ux, uy, uz;
+    if (fabs(vx) > fabs(vy)) {
+        const double s = 1.0 / sqrt(vx * vx + vz * vz);
+        ux = -vz * s, uy = 0.0, uz = vx * s;
+    } else {
+        const double s = 1.0 / sqrt(vy * vy + vz * vz);
+        ux = 0.0, uy = vz * s, uz = -vy * s;
+    }
+    const double wx = vy * uz - vz * uy, wy = vz * ux - vx * uz, wz = vx * uy - vy * ux;
+    // the 2x2 block [[al ga][ga be]] of E on that plane
+    const double e1x = aq * ux + d * uy + e * uz, e1y = d * ux + bq * uy + f * uz, e1z = e * ux + f * uy + cq * uz;
+    const double e2x = aq * wx + d * wy + e * wz, e2y = d * wx + bq * wy + f * wz, e2z = e * wx + f * wy + cq * wz;
+    const double al = ux * e1x + uy * e1y + uz * e1z;
+    const double be = wx * e2x + wy * e2y + wz * e2z;
+    const double ga = ux * e2x + uy * e2y + uz * e2z;
+    const double h = (al - be) * 0.5;
+    return (al + be) * 0.5 - sqrt(h * h + ga * ga);
+}
+
+template <bool REFINE = false>
 __device__ __forceinline__ double eigmin3(double a, double b, double c, double d, double e, double f) {
     const double p1 = d * d + e * e + f * f;
     if (p1 == 0.0) return fmin(a, fmin(b, c));
@@ -2006,6 +2054,9 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     r = fmin(1.0, fmax(-1.0, r));
     // u = sqrt(w), w in [0, 1], the same way (w floored at 1e-290: u < 1e-145 reads as 0)
     const double w = fmax((1.0 - r) * 0.5, 1e-290);
+    if constexpr (REFINE) {
+        if (w < 1e-6) return q + eigmin3_deflate(aq, bq, cq, d, e, f, p, w);
+    }
     double iu = __builtin_amdgcn_rsq(w);
     iu = iu * (1.5 - 0.5 * w * iu * iu);
     iu = iu * (1.5 - 0.5 * w * iu * iu);
@@ -2042,7 +2093,7 @@ __device__ __forceinline__ void k5_solve_store(const F (&acc)[9][K5_R], int z0l,
         vx[o] = (F)ox;
         vy[o] = (F)oy;
         vz[o] = (F)oz;
-        rel[o] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
+        rel[o] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
     }
 }
 
@@ -2362,7 +2413,7 @@ __global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float
             vx[o + e] = (float)ox;
             vy[o + e] = (float)oy;
             vz[o + e] = (float)oz;
-            rel[o + e] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
+            rel[o + e] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
         }
     }
 }
@@ -2422,6 +2473,15 @@ __global__ __launch_bounds__(256) void k_prod_gen(const F* __restrict__ G, F* __
             P[p * fs + i] = G[((pa >> (4 * p)) & 15u) * fs + i] * G[((pb >> (4 * p)) & 15u) * fs + i];
 }
 
+// Reliability of given structure tensors (of3d_rel3d): field-major [6][n] in the order
+// x2 y2 z2 xy xz yz, the same eigmin3 instance the solve kernels use for RelT
+template <typename RelT>
+__global__ __launch_bounds__(256) void k_rel3d(const double* __restrict__ T, size_t n, RelT* __restrict__ rel) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        rel[i] = (RelT)eigmin3<std::is_same_v<RelT, double>>(T[i], T[n + i], T[2 * n + i], T[3 * n + i],
+                                                             T[4 * n + i], T[5 * n + i]);
+}
+
 // 3D solve + reliability from the nine windowed fields (order tx ty tz xy xz x2 yz y2 z2)
 template <typename F, typename RelT>
 __global__ __launch_bounds__(256) void k_solve3_gen(const F* __restrict__ W, size_t fs, size_t n, F* __restrict__ vx,
@@ -2434,7 +2494,7 @@ __global__ __launch_bounds__(256) void k_solve3_gen(const F* __restrict__ W, siz
         vx[i] = (F)ox;
         vy[i] = (F)oy;
         vz[i] = (F)oz;
-        rel[i] = (RelT)eigmin3(x2, y2, z2, xy, xz, yz);
+        rel[i] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
     }
 }
 

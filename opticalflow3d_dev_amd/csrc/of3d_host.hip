@@ -1633,6 +1633,20 @@ int of3d_flow_stats(const void* vx, const void* vy, const void* vz, const void* 
     return 0;
 }
 
+int of3d_rel3d(const double* tensor, int64_t n, void* rel, int rel_f64, void* stream) {
+    if (n < 0) return fail("of3d: negative element count");
+    if (n == 0) return 0;
+    if (!tensor || !rel) return fail("of3d: null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 32);
+    if (rel_f64)
+        hipLaunchKernelGGL(k_rel3d<double>, dim3(blocks), dim3(256), 0, s, tensor, (size_t)n, (double*)rel);
+    else
+        hipLaunchKernelGGL(k_rel3d<float>, dim3(blocks), dim3(256), 0, s, tensor, (size_t)n, (float*)rel);
+    OF3D_HIP(hipGetLastError());
+    return 0;
+}
+
 int of3d_copy_async(void* dst, const void* src, size_t bytes, int max_blocks, void* stream) {
     if (bytes == 0) return 0;
     if (!dst || !src) return fail("of3d: null argument");

@@ -45,6 +45,30 @@ def rand_u16(shape, seed, hi=4096):
     return np.random.default_rng(seed).integers(0, hi, size=shape).astype(np.uint16)
 
 
+def ramp_u16(shape, axes, slope, speed):
+    """I(t, z, y, x) = 1000 + slope * (a_x x + a_y y + a_z z) + speed * t (uint16)."""
+    nt, nz, ny, nx = shape
+    t, z, y, x = np.meshgrid(*(np.arange(n, dtype=np.float64) for n in shape), indexing="ij")
+    ax, ay, az = axes
+    return np.round(1000 + slope * (ax * x + ay * y + az * z) + speed * t).astype(np.uint16)
+
+
+def wave_u16(shape, k, freq, speed):
+    """A plane wave 2000 + 900 sin(freq (k . (x, y, z)) + speed t) (uint16)."""
+    t, z, y, x = np.meshgrid(*(np.arange(n, dtype=np.float64) for n in shape), indexing="ij")
+    return np.round(2000 + 900 * np.sin(freq * (k[0] * x + k[1] * y + k[2] * z) + speed * t)).astype(np.uint16)
+
+
+def smooth_noise_u16(shape, seed):
+    """White noise smoothed by an isotropic Gaussian in z, y, x (sigma 2), per frame."""
+    from scipy.ndimage import gaussian_filter
+
+    rng = np.random.default_rng(seed)
+    noise = rng.standard_normal(shape)
+    sm = np.stack([gaussian_filter(f, 2.0, mode="wrap") for f in noise])
+    return np.round(2000 + 800 * sm / sm.std()).astype(np.uint16)
+
+
 CASES_3D = [
     # name, input builder, (sig, tsig, wsig)
     ("c3d_rand_s1", lambda: rand_u16((7, 6, 20, 24), 1), (1, 1, 2)),
@@ -69,6 +93,15 @@ CASES_3D = [
     # W radii 9 and 18 (wSig 3, 6): the fused K34 / K5c instances added for them
     ("c3d_wsig3", lambda: rand_u16((7, 6, 36, 40), 16), (2, 1, 3)),
     ("c3d_wsig6", lambda: rand_u16((7, 9, 44, 48), 17), (1, 1, 6)),
+    # round 4: near-degenerate structure tensors (the fp64 rel's hard case: the two smallest
+    # eigenvalues (nearly) equal) — a moving linear ramp along x+y+z (rank-1 tensor: lambda_min
+    # = lambda_mid ~ 0 in the interior), a ramp and a plane wave in the xy plane (z2 = 0), and
+    # isotropically smoothed noise (near-isotropic tensors); the plain trigonometric form misses
+    # 1e-10 lambda_max on the planar ramp (5.7e-9 at 11 % of its voxels) and wave (3.3e-10)
+    ("c3d_ramp_xyz_rank1", lambda: ramp_u16((7, 10, 24, 28), (1, 1, 1), 30, -25), (1, 1, 3)),
+    ("c3d_ramp_xy_planar", lambda: ramp_u16((7, 10, 24, 28), (1, 3, 0), 14, 5), (1, 1, 2)),
+    ("c3d_wave_planar", lambda: wave_u16((7, 10, 24, 28), (1, 2, 0), 0.35, -0.3), (1, 1, 3)),
+    ("c3d_iso_smoothed_noise", lambda: smooth_noise_u16((7, 12, 30, 32), 18), (1, 1, 4)),
 ]
 
 CASES_2D = [

@@ -200,3 +200,36 @@ def test_zslabs_general_path(general_path):
     for world in (2, 3):
         vx, vy, vz, rel = flow3d_zslabs_host(g["images"], g["sig"], g["tsig"], g["wsig"], world)
         assert bits_equal(vx, g["vx"]) and bits_equal(vy, g["vy"]) and bits_equal(vz, g["vz"])
+
+
+@pytest.mark.parametrize("psd", [False, True])
+def test_rel3d_device_formula_near_degenerate(psd):
+    """The device eigenvalue (of3d_rel3d: the eigmin3 instance the flow kernels store) on
+    tools/eig_poly.py's sets — generic, near-degenerate, exact pairs, near-degenerate smallest
+    pair, near-isotropic, rank 1 — against fp64 eigvalsh: fp64 rel <= 1e-10 lambda_max (the
+    deflation branch), float32 rel <= 1e-6 lambda_max."""
+    import os
+    import sys
+
+    import torch
+
+    from conftest import REPO
+    from opticalflow3d_dev_amd import _lib
+
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import eig_poly
+
+    args, ref = eig_poly.test_set(n=120000, seed=5, psd=psd)
+    lmax = np.abs(ref).max(axis=1)
+    dev = torch.device("cuda", 0)
+    t = torch.from_numpy(np.ascontiguousarray(np.stack(args))).to(dev)
+    lib = _lib.load()
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for f64, tol in ((1, REL_TOL_FP64), (0, REL_TOL_REF)):
+        out = torch.empty(len(lmax), dtype=torch.float64 if f64 else torch.float32, device=dev)
+        _lib.check(lib.of3d_rel3d(t.data_ptr(), len(lmax), out.data_ptr(), f64, s))
+        torch.cuda.synchronize(dev)
+        err = np.abs(out.cpu().numpy().astype(np.float64) - ref[:, 0]) / lmax
+        assert err.max() <= tol, (f64, err.max())
+        if f64:
+            assert err.max() <= 1e-12, err.max()
