@@ -172,7 +172,9 @@ int of3d_plan_execute_next(of3d_plan* plan, const void* const* d_frames, const v
  * min(n_ahead, 4) + 1: 2rt+m frame reads for m derivatives instead of m(2rt+1)); the later
  * of3d_plan_execute_ahead calls for exactly those windows (frame pointers, dtype, frame_z0,
  * planes) skip their K0.  Calls on one stream (or otherwise ordered); any other execute call
- * drops the formed derivatives.  Bit-identical to of3d_plan_execute. */
+ * drops the formed derivatives.  n_ahead past 65 - (2rt+1) frames is clamped (no batching
+ * beyond the 65-frame pointer table); radii without a batched K0 instance (rt other than
+ * 3, 6, 9) run the plain K0.  Bit-identical to of3d_plan_execute. */
 int of3d_plan_execute_ahead(of3d_plan* plan, const void* const* d_frames, int n_ahead, int dtype, int64_t frame_z0,
                             int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz, void* d_rel,
                             void* stream);

@@ -317,8 +317,8 @@ def process_flow(imDir, imName, fileType="SequenceT", spatialDimensions=3, xyzSi
     if axis is not None:
         if fileType == 'OneTif' and allImages is not None:
             load_rows = lambda i, y0, y1: np.asarray(allImages[i][:, y0:y1])
-        elif fileType == 'OneTif':
-            load_rows = lambda i, y0, y1: load_frame(i)[:, y0:y1]
+        elif fileType == 'OneTif':  # compressed / tiled: only the strips holding the rows
+            load_rows = lambda i, y0, y1: one.read_rows(y0, y1, pages=(i * int(Nz), (i + 1) * int(Nz)))
         else:
             load_rows = lambda i, y0, y1: tf.TiffFile(imDir / fileList[i]).read_rows(y0, y1)
         _process_slab(load_planes if axis == 0 else load_rows, axis, (int(Nz), int(Ny), int(Nx)), nOut, NtChunk,

@@ -86,6 +86,7 @@ struct of3d_plan {
     const void* pipe_frames[kMaxT] = {};
     int64_t pipe_fz0 = 0, pipe_zo0 = 0, pipe_zo1 = 0;
     int pipe_dtype = 0;
+    bool pipe_k12 = false;  // the producing call's flow (dt0 in Y4 with K12, else Y0)
     // K0 batching (of3d_plan_execute_ahead): dt0 slots Y4 .. Y4 + kDtSlots - 1 (K12 flow, whose
     // workspace leaves Y4..Y8 free), each tagged with the window it was formed for; the call
     // that uses a slot consumes it, and any other call drops them all
@@ -809,6 +810,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         for (auto& d : p->dts) d.valid = false;
     }
     // field buffers
+    // a pipelined dt0 lives where the producing call's flow put it (Y4 with K12, else Y0): whether
+    // a call runs K12 is decided per call (alignment, OF3D_K12), so the flows must agree
+    if (skip_k0 && pipe && p->pipe_k12 != (k12 != nullptr)) skip_k0 = false;
     F* D0b = k12 ? Y + (4 + dslot) * fs : Y;  // temporal derivative (K0 -> K1 / K12), origin zb0
     k0n.D0 = D0b;
     F* Bb = d3 ? Y + 4 * fs : X;       // pre-z fields (3D) / final gradients (2D), origin zb0
@@ -1098,6 +1102,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             p->pipe_zo0 = zo0;
             p->pipe_zo1 = zo1;
             p->pipe_dtype = dtype;
+            p->pipe_k12 = k12 != nullptr;
         }
     } else {
         // overlap: chunk c = outputs [o_c, o_c+1); its G/Q planes end rw above, its B planes rd above that
@@ -1201,8 +1206,14 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     // candidate and compare bits; multi-rank runs can pin one choice for every rank)
     if (const char* e = getenv("OF3D_K34_CAND"); e && e[0]) {
         const size_t i = (size_t)atoll(e);
-        if (i >= p->k34_cand.size()) return fail("of3d: OF3D_K34_CAND out of range");
-        p->k34 = p->k34_cand[i];
+        if (i < p->k34_cand.size()) {
+            p->k34 = p->k34_cand[i];
+        } else {  // a pin meant for another plan shape (fewer candidates): keep the heuristic pick
+            const char* st = getenv("OF3D_K34_CAND_STRICT");
+            if (st && st[0] == '1') return fail("of3d: OF3D_K34_CAND out of range");
+            fprintf(stderr, "of3d: OF3D_K34_CAND=%zu ignored for this plan (%zu candidates)\n", i,
+                    p->k34_cand.size());
+        }
     } else if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
         OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
         OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
@@ -1466,7 +1477,8 @@ int of3d_plan_execute_next(of3d_plan* p, const void* const* d_frames, const void
 int of3d_plan_execute_ahead(of3d_plan* p, const void* const* d_frames, int n_ahead, int dtype, int64_t frame_z0,
                             int64_t zo0, int64_t zo1, void* vx, void* vy, void* vz, void* rel, void* stream) {
     if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
-    if (n_ahead < 0 || 2 * p->rt + 1 + n_ahead > kMaxT) return fail("of3d: n_ahead out of range");
+    if (n_ahead < 0) return fail("of3d: n_ahead out of range");
+    n_ahead = std::min(n_ahead, kMaxT - (2 * p->rt + 1));  // frames past kMaxT are not batched
     OF3D_HIP(hipSetDevice(p->device));
     hipStream_t s = stream ? (hipStream_t)stream : p->stream;
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, nullptr, false, n_ahead);

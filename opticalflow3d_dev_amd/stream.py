@@ -26,6 +26,9 @@ import numpy as np
 from . import _lib
 from .taps import make_taps, radii
 
+K0_BATCH_RADII = (3, 6, 9)  # temporal radii with a batched K0 instance (csrc/kt_grad.hip k0m_fn)
+MAX_FRAMES = 65  # frame pointers per plan call (kMaxT in csrc/of3d_host.hip)
+
 # torch storage type holding each kernel-native input dtype (same width; the kernels read the bits)
 _TORCH_VIEW = {
     np.dtype(np.uint8): "uint8",
@@ -92,9 +95,14 @@ class FlowStream:
         self.batch = 0
         if k0_batch is None:  # default: K0 batching of 5 windows for whole-volume 3D streams
             k0_batch = 5 if lookahead is None else 0
-        if k0_batch >= 2 and ndim == 3 and zslab is None:
+        # batched K0 instances exist for rt 3, 6, 9 (tSig 1, 2, 3: csrc/kt_grad.hip k0m_fn) and
+        # 2rt+M frames within the plan's 65-frame table; elsewhere the ring holds no lookahead
+        if (k0_batch >= 2 and ndim == 3 and zslab is None and self.rt in K0_BATCH_RADII
+                and self.nwin + min(int(k0_batch), 5) - 1 <= MAX_FRAMES):
             self.batch = min(int(k0_batch), 5)
             lookahead = False
+        elif k0_batch >= 2 and lookahead is None:
+            lookahead = False  # asked for batching: no frame pipelining in its place
         if lookahead is None:
             lookahead = ndim == 3 and zslab is None
         self.L = self.batch - 1 if self.batch else (1 if lookahead else 0)

@@ -121,10 +121,12 @@ class TiffFile:
                 raise ValueError(f"{self.path}: bad TIFF magic {magic}")
             self.byteorder = bo
             self.pages = []
+            self.ifd_offsets = []  # file offset of each page's IFD (libtiff jumps straight to one)
             seen = set()
             off = first
             while off and off not in seen:
                 seen.add(off)
+                self.ifd_offsets.append(off)
                 tags, off = self._read_ifd(f, off)
                 self.pages.append(Page(tags, bo))
         self.imagej_metadata = _parse_imagej(self.pages[0].description) if self.pages else None
@@ -232,8 +234,8 @@ class TiffFile:
         bytes are read when the pages are uncompressed, only those pages decoded otherwise."""
         p0 = self.pages[0]
         if self._needs_codec():
-            arr = imread_libtiff(self.path, pages=(z0, z1)).reshape((z1 - z0,) + p0.shape)
-            return np.ascontiguousarray(arr, dtype=p0.dtype.newbyteorder("="))
+            arr = imread_libtiff(self.path, pages=(z0, z1), ifd_offset=self.ifd_offsets[z0])
+            return np.ascontiguousarray(arr.reshape((z1 - z0,) + p0.shape), dtype=p0.dtype.newbyteorder("="))
         blk = self._contiguous_block()
         out = np.empty((z1 - z0,) + p0.shape, p0.dtype.newbyteorder("="))
         with open(self.path, "rb") as f:
@@ -249,14 +251,19 @@ class TiffFile:
                 out[k] = np.frombuffer(b"".join(chunks), dtype=p.dtype)[: int(np.prod(p.shape))].reshape(p.shape)
         return out
 
-    def read_rows(self, y0, y1):
-        """Rows [y0, y1) of every page of a plain page series, as (pages, y1 - y0, x)."""
+    def read_rows(self, y0, y1, pages=None):
+        """Rows [y0, y1) of every page (or of pages=(p0, p1): a OneTif frame's planes) of a
+        plain page series, as (pages, y1 - y0, x)."""
         p0 = self.pages[0]
+        a, b = pages if pages is not None else (0, len(self.pages))
         blk = self._contiguous_block()
         if blk is not None and not self._needs_codec():
             mm = np.memmap(self.path, dtype=p0.dtype, mode="r", offset=blk[0], shape=(len(self.pages),) + p0.shape)
-            return np.ascontiguousarray(mm[:, y0:y1], dtype=p0.dtype.newbyteorder("="))
-        return np.ascontiguousarray(self.read_planes(0, len(self.pages))[:, y0:y1])
+            return np.ascontiguousarray(mm[a:b, y0:y1], dtype=p0.dtype.newbyteorder("="))
+        if self._needs_codec():  # decode only the strips / tile rows that hold rows [y0, y1)
+            arr = imread_libtiff(self.path, pages=(a, b), ifd_offset=self.ifd_offsets[a], rows=(y0, y1))
+            return np.ascontiguousarray(arr, dtype=p0.dtype.newbyteorder("="))
+        return np.ascontiguousarray(self.read_planes(a, b)[:, y0:y1])
 
     def asarray(self):
         blk = self._contiguous_block()
@@ -512,6 +519,8 @@ def _libtiff():
         lib.TIFFReadDirectory.restype = ctypes.c_int
         lib.TIFFSetDirectory.argtypes = [P, ctypes.c_uint32]
         lib.TIFFSetDirectory.restype = ctypes.c_int
+        lib.TIFFSetSubDirectory.argtypes = [P, ctypes.c_uint64]
+        lib.TIFFSetSubDirectory.restype = ctypes.c_int
         lib.TIFFClose.argtypes = [P]
         lib.TIFFClose.restype = None
         lib.TIFFIsTiled.argtypes = [P]
@@ -537,10 +546,11 @@ def imwrite_matlab(path, data):
     imwrite_libtiff(path, data, compression=5, bigtiff=True)
 
 
-def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, tile=None):
+def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, tile=None, rows_per_strip=None):
     """One page per plane through the system libtiff: ``compression`` (5 LZW, 8 deflate,
-    1 none), optional ImageDescription, strips of libtiff's default size or ``tile``
-    (th, tw) tiles (multiples of 16).  Integer or float samples."""
+    1 none), optional ImageDescription, strips of libtiff's default size (or
+    ``rows_per_strip`` rows) or ``tile`` (th, tw) tiles (multiples of 16).  Integer or float
+    samples."""
     import ctypes
 
     lib = _libtiff()
@@ -569,7 +579,7 @@ def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, t
                 lib.TIFFSetField(ctypes.c_void_p(tif), U32(270), ctypes.c_char_p(description.encode("latin-1")))
             plane = arr[z]
             if tile is None:
-                rps = int(lib.TIFFDefaultStripSize(tif, 0))
+                rps = int(rows_per_strip or lib.TIFFDefaultStripSize(tif, 0))
                 lib.TIFFSetField(ctypes.c_void_p(tif), U32(T["ROWSPERSTRIP"]), U32(rps))
                 row_bytes = nx * arr.itemsize
                 for s, r0 in enumerate(range(0, ny, rps)):
@@ -595,10 +605,13 @@ def imwrite_libtiff(path, data, compression=5, bigtiff=True, description=None, t
         lib.TIFFClose(tif)
 
 
-def imread_libtiff(path, pages=None):
+def imread_libtiff(path, pages=None, ifd_offset=None, rows=None):
     """Read any single-sample TIFF libtiff can decode (e.g. the LZW BigTIFFs of
     imwrite_matlab / MATLAB's TIFFwrite) as a (pages, y, x) or (y, x) array.
-    pages=(p0, p1): decode only pages [p0, p1) (always a (p1 - p0, y, x) array)."""
+    pages=(p0, p1): decode only pages [p0, p1) (always a (p1 - p0, y, x) array);
+    ifd_offset: the file offset of page p0's IFD (TiffFile.ifd_offsets) — libtiff then
+    jumps to it instead of walking the p0 directories before it; rows=(y0, y1): only
+    those rows of each page, decoding only the strips / tile rows that hold them."""
     import ctypes
 
     lib = _libtiff()
@@ -607,7 +620,9 @@ def imread_libtiff(path, pages=None):
         raise OSError("libtiff could not open " + str(path))
     if pages is not None:
         p0, p1 = pages
-        if p1 <= p0 or not lib.TIFFSetDirectory(tif, p0):
+        ok = p1 > p0 and (lib.TIFFSetSubDirectory(tif, ifd_offset) if ifd_offset is not None
+                          else lib.TIFFSetDirectory(tif, p0))
+        if not ok:
             lib.TIFFClose(tif)
             raise ValueError(f"{path}: no pages [{p0}, {p1})")
     T = _TIFFTAG
@@ -619,26 +634,31 @@ def imread_libtiff(path, pages=None):
             w, h = get(T["IMAGEWIDTH"], ctypes.c_uint32), get(T["IMAGELENGTH"], ctypes.c_uint32)
             bits, fmt = get(T["BITSPERSAMPLE"], ctypes.c_uint16), get(T["SAMPLEFORMAT"], ctypes.c_uint16) or 1
             dt = np.dtype({1: "u", 2: "i", 3: "f"}[fmt] + str(bits // 8))
-            out = np.empty((h, w), dt)
-            buf = out.reshape(-1).view(np.uint8)
-            pos = 0
-            for s in range(0 if lib.TIFFIsTiled(tif) else lib.TIFFNumberOfStrips(tif)):
-                n = lib.TIFFReadEncodedStrip(tif, s, buf[pos:].ctypes.data, buf.size - pos)
-                if n < 0:
-                    raise OSError("libtiff failed decoding " + str(path))
-                pos += n
-            buf = out.reshape(-1).view(np.uint8)
+            y0, y1 = rows if rows is not None else (0, h)
             if lib.TIFFIsTiled(tif):
                 tw, th = get(T["TILEWIDTH"], ctypes.c_uint32), get(T["TILELENGTH"], ctypes.c_uint32)
+                r0 = (y0 // th) * th
+                out = np.empty((min(-(-y1 // th) * th, h) - r0, w), dt)
                 tile = np.empty((th, tw), dt)
-                for ty in range(0, h, th):
+                for ty in range(r0, y1, th):
                     for tx in range(0, w, tw):
                         n = lib.TIFFReadEncodedTile(tif, lib.TIFFComputeTile(tif, tx, ty, 0, 0), tile.ctypes.data,
                                                     tile.nbytes)
                         if n < 0:
                             raise OSError("libtiff failed decoding " + str(path))
-                        out[ty:ty + th, tx:tx + tw] = tile[:min(th, h - ty), :min(tw, w - tx)]
-            planes.append(out)
+                        out[ty - r0:ty - r0 + th, tx:tx + tw] = tile[:min(th, h - ty), :min(tw, w - tx)]
+            else:
+                rps = min(get(T["ROWSPERSTRIP"], ctypes.c_uint32) or h, h)
+                r0 = (y0 // rps) * rps
+                out = np.empty((min(-(-y1 // rps) * rps, h) - r0, w), dt)
+                buf = out.reshape(-1).view(np.uint8)
+                pos = 0
+                for st in range(y0 // rps, -(-y1 // rps)):
+                    n = lib.TIFFReadEncodedStrip(tif, st, buf[pos:].ctypes.data, buf.size - pos)
+                    if n < 0:
+                        raise OSError("libtiff failed decoding " + str(path))
+                    pos += n
+            planes.append(out[y0 - r0:y1 - r0])
             if (pages is not None and len(planes) == pages[1] - pages[0]) or not lib.TIFFReadDirectory(tif):
                 break
     finally:

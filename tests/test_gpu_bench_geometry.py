@@ -139,12 +139,13 @@ def test_c3_full_size_vs_oracle_crops(c3, crop):
 
 
 def k34_candidates(d_in, p, mode=0):
-    """Number of K34 autotune candidates of this plan shape (OF3D_K34_CAND past the end fails)."""
+    """Number of K34 autotune candidates of this plan shape (OF3D_K34_CAND past the end fails with
+    OF3D_K34_CAND_STRICT=1; without it a pin past the end is ignored with a warning)."""
     from opticalflow3d_dev_amd import _lib, make_taps
 
     n = 0
     while n < 64:
-        with env(OF3D_K34_CAND=n):
+        with env(OF3D_K34_CAND=n, OF3D_K34_CAND_STRICT=1):
             try:
                 _lib.Plan(3, p["nz"], p["ny"], p["nx"], make_taps(p["s"], p["t"], p["w"]), device=0,
                           mode=mode).close()

@@ -252,3 +252,51 @@ def test_zslab_subrange_batched(z0, z1):
         assert "k_tderiv_multi" in plan.kernels(), plan.kernels()
     finally:
         plan.close()
+
+
+@pytest.mark.parametrize("tsig", [10.5, 1.5])
+def test_flowstream_unbatchable_radius(tsig):
+    """Temporal radii without a batched K0 (rt 32 = tSig 10.5: a 65-frame window, the plan's
+    whole frame table; rt 5 = tSig 1.5: no k_tderiv_multi instance): the stream holds no
+    lookahead and runs the plain K0, every output equal to calc_flow3D of its window."""
+    from opticalflow3d_dev_amd.stream import FlowStream
+
+    s, w = 1, 2
+    shape = (6, 20, 24)
+    rt = radii(s, tsig, w)[2]
+    nwin = 2 * rt + 1
+    stack = np.random.default_rng(19).integers(0, 3000, size=(nwin + 2,) + shape).astype(np.uint16)
+    fs = FlowStream(3, shape, np.uint16, s, tsig, w, depth=1)
+    try:
+        assert fs.batch == 0 and fs.L == 0, (fs.batch, fs.L)
+        k = 0
+        for i in range(stack.shape[0]):
+            fs.push(stack[i])
+            while len(fs.order) >= fs.nwin + fs.L or (i == stack.shape[0] - 1 and fs.ready):
+                p = fs.submit()
+                for a, b in zip(p.result(), calc_flow3D(stack[k:k + nwin], s, tsig, w)):
+                    assert bits_equal(a, b), k
+                p.release()
+                k += 1
+        assert k == 3
+        assert "k_tderiv_multi" not in fs.plan.kernels()
+    finally:
+        fs.close()
+
+
+def test_execute_ahead_clamps_past_frame_table():
+    """of3d_plan_execute_ahead with more lookahead than the 65-frame table holds: clamped, not
+    an error (rt 30: a 61-frame window leaves 4 frames of lookahead), and exact."""
+    import torch
+
+    s, t, w = 1, 10, 2
+    rt = radii(s, t, w)[2]
+    nwin = 2 * rt + 1
+    stack, frames = _series(nwin + 6, s, t, w, 20, shape=(NZ, NY, NX))
+    plan = _lib.Plan(3, NZ, NY, NX, make_taps(s, t, w), device=0)
+    try:
+        got = _call(plan, frames, 0, nwin, 6, torch.float64, torch.float32)
+        for a, b in zip(got, calc_flow3D(stack[:nwin], s, t, w)):
+            assert bits_equal(a, b)
+    finally:
+        plan.close()

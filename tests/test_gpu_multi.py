@@ -167,10 +167,11 @@ def test_sequencet_yslab_two_ranks(tmp_path):
 @pytest.mark.parametrize("world,parallel", [(1, "auto"), (2, "zslab"), (2, "yslab")])
 def test_lzw_onetif_multi_rank(tmp_path, world, parallel):
     """An LZW-compressed hyperstack split over ranks: every rank decodes only the pages of
-    its planes (tiff.imread_libtiff page ranges), results equal the oracle."""
+    its planes (tiff.imread_libtiff page ranges; row slabs: only the strips holding its rows),
+    results equal the oracle."""
     stack = np.random.default_rng(16).integers(0, 4096, size=(7, 6, 18, 22)).astype(np.uint16)
     tf.imwrite_libtiff(tmp_path / "q.tif", stack.reshape(-1, 18, 22), compression=5, bigtiff=False,
-                       description=tf.imagej_description(stack.shape))
+                       description=tf.imagej_description(stack.shape), rows_per_strip=4)
     if world == 1:
         process_flow(str(tmp_path), "q", "OneTif", 3, 1, 1, 2)
     else:

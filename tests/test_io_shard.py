@@ -151,6 +151,31 @@ def test_read_rows(tmp_path):
     assert np.array_equal(tf.TiffFile(tmp_path / "c.tif").read_rows(0, 5), a[:, 0:5])
 
 
+@pytest.mark.parametrize("layout", ["strips4", "strips7", "tiles"])
+def test_read_rows_decodes_only_their_strips(tmp_path, layout):
+    """Row slabs of compressed pages (process_flow's row-slab ranks): every row window equals
+    the full decode, for windows inside one strip / tile row, across several, at both edges."""
+    a = np.random.default_rng(6).integers(0, 60000, (3, 45, 40)).astype(np.uint16)
+    kw = dict(tile=(16, 32)) if layout == "tiles" else dict(rows_per_strip=int(layout[6:]))
+    tf.imwrite_libtiff(tmp_path / "c.tif", a, compression=8, bigtiff=False, **kw)
+    t = tf.TiffFile(tmp_path / "c.tif")
+    assert np.array_equal(t.asarray(), a)
+    for y0, y1 in ((0, 45), (0, 1), (3, 4), (4, 8), (5, 30), (17, 33), (44, 45), (31, 45)):
+        assert np.array_equal(t.read_rows(y0, y1), a[:, y0:y1]), (y0, y1)
+        assert np.array_equal(t.read_rows(y0, y1, pages=(1, 3)), a[1:3, y0:y1]), (y0, y1)
+
+
+def test_page_ranges_jump_to_their_ifd(tmp_path):
+    """read_planes on compressed pages opens libtiff at the first page's IFD offset (no walk over
+    the earlier directories): every page range of a long page series decodes exactly."""
+    a = np.random.default_rng(7).integers(0, 4096, (40, 9, 13)).astype(np.uint16)
+    tf.imwrite_libtiff(tmp_path / "c.tif", a, compression=5, bigtiff=True)
+    t = tf.TiffFile(tmp_path / "c.tif")
+    assert len(t.ifd_offsets) == 40
+    for z0, z1 in ((0, 1), (39, 40), (12, 20), (0, 40), (25, 26)):
+        assert np.array_equal(t.read_planes(z0, z1), a[z0:z1])
+
+
 def test_slab_axis_prefers_rows_for_flat_volumes():
     from opticalflow3d_dev_amd.shard import slab_axis, slab_work
 
