@@ -384,6 +384,7 @@ class SlabBench:
         nz, ny, nx = dims
         s, t, w = sig
         self.dims, self.axis, self.rank, self.world, self.dev = dims, axis, rank, world, dev
+        self.sig, self.seed = (s, t, w), seed
         self.rd, self.rs, self.rt, self.rw = radii(s, t, w)
         self.nwin = 2 * self.rt + 1
         self.fp32 = fp32
@@ -433,6 +434,7 @@ class SlabBench:
         self.xev = {}   # slot -> event of its frame's halo exchange (not yet waited for)
         self.order = list(range(self.nwin + self.L))  # the window (+ the lookahead frames)
         self.k = 0  # steps computed (K0 batching: step k % M == 0 forms M windows' dt0)
+        self.last_window = None  # ring slots of the last computed window (slot f holds seed + f)
 
     def _xchg_view(self, slot):
         v = self.ring[slot]
@@ -473,6 +475,7 @@ class SlabBench:
                 self.comp.wait_event(self.xev.pop(sl))
         if compute:
             window = self.order[:self.nwin]
+            self.last_window = list(window)
             ptrs = [self.ring[sl].data_ptr() for sl in window]
             nxt = [self.ring[sl].data_ptr() for sl in self.order[1:]] if self.L and not self.batch else None
             ahead = [self.ring[sl].data_ptr() for sl in self.order[self.nwin:]] if self.batch else None
@@ -528,52 +531,180 @@ def timed_steps(step, steps, warmup, world, dev):
     return max_over_ranks([el], dev)[0] if world > 1 else el
 
 
-def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=True, k0_batch=0):
-    """The default workload's frame split over the N ranks (strong scaling) — the path
-    configs[3]/[4] and process_flow(parallel="zslab"/"yslab") run, on the headline volume:
-    per-rank compute alone, the halo exchange alone (RCCL P2P of the newest frame's rd + rw
-    planes / rows), and the pipelined step (exchange beside the previous step's compute).
-    efficiency = the one-GPU frame time t1 (this run's replica step) / (N * step)."""
+def slab_parity(sb, fp32):
+    """parity_sample of a slab run (every rank calls it; rank 0 returns the result, the others
+    None): one 16^3 output crop straddling the cut between rank 0 and rank 1 on the split axis
+    (the volume centre on one GPU), its planes / rows gathered from their owner ranks, checked on
+    rank 0 against the oracle of the crop's input box — regenerated from the synthetic family
+    the ranks generated their parts from (synthetic_slab: values are a function of the global
+    coordinates and the frame's seed), for the frames of the last computed window."""
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd.shard import zslab_bounds
+
+    nz, ny, nx = sb.dims
+    dims = (nz, ny, nx)
+    world = 1 if sb.vrank else sb.world
+    n_ax = dims[sb.axis]
+    cut = zslab_bounds(n_ax, 0, world)[1] if world > 1 else n_ax // 2
+    ctr = [nz // 2, ny // 2, nx // 2 + 44]
+    ctr[sb.axis] = cut
+    box = []
+    for c, n in zip(ctr, dims):
+        a = min(max(c - 8, 0), max(n - 16, 0))
+        box += [a, min(a + 16, n)]
+    z0, z1, y0, y1, x0, x1 = box
+    # this rank's own outputs inside the box: 4 outputs + an ownership mask, as float64
+    crop = torch.zeros((5, z1 - z0, y1 - y0, x1 - x0), dtype=torch.float64, device=sb.dev)
+    b0, b1 = (z0, z1) if sb.axis == 0 else (y0, y1)
+    o0, o1 = max(b0, sb.a0), min(b1, sb.a1)
+    if o1 > o0 and sb.n_out:
+        for k, o in enumerate(sb.outs + [sb.rel]):
+            if sb.axis == 0:
+                v = o[:sb.n_out].view(sb.a1 - sb.a0, ny, nx)[o0 - sb.a0:o1 - sb.a0, y0:y1, x0:x1]
+                crop[k, o0 - z0:o1 - z0] = v.double()
+            else:
+                r0 = sb.a0 if sb.rows_direct else sb.ai0
+                rows = (sb.a1 - sb.a0) if sb.rows_direct else (sb.ai1 - sb.ai0)
+                v = o[:sb.n_out].view(nz, rows, nx)[z0:z1, o0 - r0:o1 - r0, x0:x1]
+                crop[k, :, o0 - y0:o1 - y0] = v.double()
+        if sb.axis == 0:
+            crop[4, o0 - z0:o1 - z0] = 1
+        else:
+            crop[4, :, o0 - y0:o1 - y0] = 1
+    if world > 1:
+        where = sb.dev if dist.get_backend() == "nccl" else "cpu"
+        mine = crop.to(where)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        if sb.rank != 0:
+            return None
+        crop = torch.zeros_like(mine)
+        for q in parts:
+            crop[:4] += q[:4] * q[4]
+            crop[4] += q[4]
+    if not bool((crop[4] == 1).all()):
+        return {"ok": False, "error": "crop voxels not owned exactly once", "crop_out": box}
+    got = [crop[k].cpu().numpy() for k in range(4)]
+    # the window's input box (crop + the rd + rw halo), regenerated on rank 0
+    h = sb.rd + sb.rw
+    lo = [max(a - h, 0) for a in (z0, y0, x0)]
+    hi = [min(b + h, n) for b, n in zip((z1, y1, x1), dims)]
+    sub = np.stack([synthetic_slab(1, nz, ny, nx, lo[0], hi[0], sb.seed + sl, sb.dev, rows=(lo[1], hi[1]))[0]
+                    [:, :, lo[2]:hi[2]].cpu().numpy().view(np.uint16) for sl in sb.last_window])
+    r = parity_check(sub, lo, box, got, *sb.sig, fp32=fp32)
+    r["where"] = ("across the cut between rank 0 and rank 1 (%s %d)" % ("plane" if sb.axis == 0 else "row", cut)
+                  if world > 1 else "volume centre")
+    return r
+
+
+def slab_on_every_rank(world, dev, *a, **kw):
+    """SlabBench(*a, **kw) on every rank, or on none: the ranks agree (a MAX over ranks) before
+    any of them starts timed steps, so a rank that cannot allocate its part (device memory)
+    does not leave the others waiting in a collective; raises on every rank then."""
+    import torch
+
+    sb, err = None, ""
+    try:
+        sb = SlabBench(*a, **kw)
+    except Exception as e:  # noqa: BLE001
+        err = f"{type(e).__name__}: {e}"[:200]
+    bad = max_over_ranks([0.0 if sb is not None else 1.0], dev)[0] if world > 1 else (0.0 if sb else 1.0)
+    if bad:
+        if sb is not None:
+            sb.close()
+        del sb
+        torch.cuda.empty_cache()
+        raise RuntimeError("slab setup failed on a rank" + (": " + err if err else ""))
+    return sb
+
+
+def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=True, k0_batch=0, fp32=False,
+                 parity=True):
+    """A volume's frame split over the N ranks (strong scaling) — the path configs[3]/[4] and
+    process_flow(parallel="zslab"/"yslab") run: per-rank compute alone, the halo exchange alone
+    (RCCL P2P of the newest frame's rd + rw planes / rows), and the pipelined step (exchange
+    beside the previous step's compute), with a parity sample across the rank-0/1 cut.
+    efficiency = the one-GPU frame time t1 (None: not measured) / (N * step)."""
     nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
-    sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, seed=20260206 + 50, pipeline=pipeline,
-                   k0_batch=k0_batch)
+    sb = slab_on_every_rank(world, dev, (nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32,
+                            seed=20260206 + 50, pipeline=pipeline, k0_batch=k0_batch)
     try:
         comp = timed_steps(lambda: sb.step(exchange=False), steps, warmup, world, dev)
         xchg = timed_steps(lambda: sb.step(compute=False), steps, warmup, world, dev)
         both = timed_steps(sb.step, steps, warmup, world, dev)
         finite = sb.finite()
         desc = sb.describe()
+        par = slab_parity(sb, fp32) if parity else None
     finally:
         sb.close()
     ms = both / steps * 1e3
     return {"split": "z-slabs" if axis == 0 else "row slabs", "halo": sb.rd + sb.rw, "rank0_part": desc,
             "ms_per_step": round(ms, 5), "value": round(nz * ny * nx / (ms * 1e-3) / 1e6, 3), "unit": "Mvoxels/s",
             "compute_ms_max_rank": round(comp / steps * 1e3, 5), "exchange_ms": round(xchg / steps * 1e3, 5),
-            "efficiency_vs_one_gpu_frame": round(t1_ms / (world * ms), 4), "outputs_finite_rank0": finite}
+            "efficiency_vs_one_gpu_frame": round(t1_ms / (world * ms), 4) if t1_ms else None,
+            "outputs_finite_rank0": finite, "parity_sample": par}
+
+
+def replica_frame(cfg, world, rank, dev, steps, warmup, fp32, pipeline, k0_batch):
+    """Every rank computes the WHOLE volume of cfg on its own GPU at once (one-GPU frames,
+    replicas): the one-GPU frame time t1 the split's efficiency is measured against, on this
+    node in this job (max over ranks), and the weak-scaling throughput of N replicas."""
+    import torch
+
+    nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
+    sb = slab_on_every_rank(world, dev, (nz, ny, nx), (s, t, w), 0, rank, world, dev, fp32=fp32, vrank=(0, 1),
+                            seed=20260206 + 60 + rank, pipeline=pipeline, k0_batch=k0_batch)
+    try:
+        el = timed_steps(sb.step, steps, warmup, world, dev)
+    finally:
+        sb.close()
+        del sb
+        torch.cuda.empty_cache()
+    ms = el / steps * 1e3
+    return {"ms_per_step": round(ms, 5), "value": round(world * nz * ny * nx / (ms * 1e-3) / 1e6, 3),
+            "unit": "Mvoxels/s", "scaling": "weak",
+            "what": f"{world} one-GPU frames at once (every rank its own whole volume), max over ranks"}
 
 
 def run_slab(args, world, rank, local_rank, dev):
-    """configs[3] / configs[4]: ONE volume per output frame, split over the ranks (strong
-    scaling) — SlabBench.  OF3D_BENCH_VRANK="r/P": time rank r of a P-way split on this one
-    GPU (no exchange) — the per-rank compute the scaling model in DESIGN.md uses."""
+    """configs[3] / configs[4], and every N > 1 line: ONE volume per output frame, split over the
+    ranks (strong scaling) — SlabBench, as process_flow(parallel="zslab") runs it.  The split
+    axis defaults to z (the north star's "volumes shard along z"); --split y / auto.  N > 1
+    also measures, beside the headline split: the one-GPU frame of the same volume on every
+    rank at once ("replicas": t1 for the efficiency) and the other axis's split ("row_slabs").
+    OF3D_BENCH_VRANK="r/P": time rank r of a P-way split on this one GPU (no exchange) — the
+    per-rank compute the scaling model in DESIGN.md uses."""
+    import torch
+
     from opticalflow3d_dev_amd import radii
     from opticalflow3d_dev_amd.shard import slab_axis
 
-    nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
+    cfg = args.config
+    nt, nz, ny, nx, s, t, w, desc = CONFIGS[cfg]
     rd, rs, rt, rw = radii(s, t, w)
     nwin = 2 * rt + 1
-    fp32 = args.config in FP32_CONFIGS or args.precision == "fp32"
+    fp32 = cfg in FP32_CONFIGS or args.precision == "fp32"
     sv = 4 if fp32 else 8
     vr = os.environ.get("OF3D_BENCH_VRANK")
     prank, pworld = (int(v) for v in vr.split("/")) if vr else (rank, world)
     axis = {"z": 0, "y": 1}.get(args.split, None)
     if axis is None:
         axis = slab_axis(nz, ny, pworld, rd, rw)
+    kb = 0 if args.no_pipeline else args.k0_batch
+    replicas = None
+    if world > 1 and not vr and not args.no_replicas:
+        try:  # the one-GPU frame first (it holds the whole volume: freed before the split)
+            replicas = replica_frame(cfg, world, rank, dev, args.steps, args.warmup, fp32, not args.no_pipeline, kb)
+        except Exception as e:  # noqa: BLE001
+            replicas = {"error": f"{type(e).__name__}: {e}"[:300]}
+            torch.cuda.empty_cache()
     seed = 20260206 + (5 if fp32 else 4)
     sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32, timing=max(args.steps, 1),
-                   vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline,
-                   k0_batch=0 if args.no_pipeline else args.k0_batch)
+                   vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline, k0_batch=kb)
     plan = sb.plan
+
     def align():
         while sb.k % sb.batch:
             sb.step()
@@ -583,45 +714,79 @@ def run_slab(args, world, rank, local_rank, dev):
     if world > 1:
         elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
         finite = bad == 0.0
+    parity = None if args.no_parity_sample or vr else slab_parity(sb, fp32)
+    split_detail = None
+    if world > 1 and not vr:  # compute alone / exchange alone on the same ranks and ring
+        comp = timed_steps(lambda: sb.step(exchange=False), args.steps, args.warmup, world, dev)
+        xchg = timed_steps(lambda: sb.step(compute=False), args.steps, args.warmup, world, dev)
+        split_detail = {"compute_ms_max_rank": round(comp / args.steps * 1e3, 5),
+                        "exchange_ms": round(xchg / args.steps * 1e3, 5),
+                        "pipelined_step_ms": round(elapsed / args.steps * 1e3, 5),
+                        "exchange": f"RCCL P2P ({'nccl' if os.environ.get('OF3D_BENCH_BACKEND', 'nccl') == 'nccl' else 'gloo rehearsal'}) "
+                                    f"of the newest frame's {rd + rw} halo {'planes' if axis == 0 else 'rows'} per "
+                                    "neighbour, on its own stream beside the previous step's compute"}
+    kernels = set(plan.kernels())
+    own, ai0, ai1, a0, a1, describe = sb.own, sb.ai0, sb.ai1, sb.a0, sb.a1, sb.describe()
+    rows_direct = sb.rows_direct
+    sb.close()
+    del sb
+    torch.cuda.empty_cache()
+    other = None
+    if world > 1 and not vr and not args.no_strong and world <= (nz, ny)[1 - axis]:
+        try:  # the other axis's split of the same volume (row slabs beside the z-slab headline)
+            t1 = replicas.get("ms_per_step") if replicas else None
+            other = strong_split(cfg, 1 - axis, world, rank, dev, args.steps, args.warmup, t1,
+                                 pipeline=not args.no_pipeline, k0_batch=kb, fp32=fp32,
+                                 parity=not args.no_parity_sample)
+        except Exception as e:  # noqa: BLE001
+            other = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0:
         vox = nz * ny * nx
-        own = sb.own
-        ai0, ai1, a0, a1 = sb.ai0, sb.ai1, sb.a0, sb.a1
         if axis == 0:
             nb, no, ng = ai1 - ai0, a1 - a0, min(a1 + rw, nz) - max(a0 - rw, 0)
             plane = ny * nx
         else:
             nb = no = ng = nz
             plane = (ai1 - ai0) * nx
-        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, plane, sv), args.config,
+        roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nb, ng, no, plane, sv), cfg,
                         (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv,
-                        used=set(plan.kernels()))
-        roof["frame"]["note"] = "this rank's share: " + sb.describe()
+                        used=kernels)
+        roof["frame"]["note"] = "this rank's share: " + describe
         cpu = None
         if world == 1 and not vr and not args.no_cpu_baseline:
             sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
             host = synthetic_slab(nwin, nz, ny, nx, 0, sub, seed, dev).cpu().numpy().view(np.uint16)
-            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
+            cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=cfg)
         split = ("z-slabs" if axis == 0 else "row slabs")
+        ms = elapsed / args.steps * 1e3
+        if split_detail is not None and replicas and "ms_per_step" in replicas:
+            split_detail["efficiency_vs_one_gpu_frame"] = round(replicas["ms_per_step"] / (world * ms), 4)
+        nres = nwin + 1 + (kb - 1 if kb >= 2 else (0 if args.no_pipeline else 1))
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round((own if vr else vox) * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
+            "ms_per_step": round(ms, 5), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32" if fp32 else "f64", "data": "synthetic",
             "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
                        "wSig": w,
                        "parallelism": (f"virtual rank {prank} of {pworld} ({split}, compute only)" if vr else
                                        f"{split} x{world}, halo {rd + rw}" if world > 1 else "single GPU (whole frame)"),
-                       "inputs": "own part of 2*rt+2 uint16 frames resident in HBM; per step the newest frame's "
-                                 "halo exchange (RCCL P2P, own stream) + compute", "outputs_finite": finite,
-                       "series": (f"K0 batching: {sb.batch} windows per K0 pass (of3d_plan_execute_ahead), "
-                                  f"ring of {sb.nwin + 1 + sb.L} frames") if sb.batch else
-                                 ("frame pipelining (of3d_plan_execute_next)" if sb.L else "plain")},
-            "roofline": roof, "cpu_baseline": cpu, "build": build_stamp(),
+                       "inputs": f"own part (+ halo) of a ring of {nres} uint16 frames resident in HBM; per step the "
+                                 "newest frame's halo exchange (RCCL P2P, own stream) + compute",
+                       "outputs_finite": finite,
+                       "row_outputs": "own rows only (of3d_plan_set_rows)" if (axis == 1 and rows_direct) else None,
+                       "series": (f"K0 batching: {kb} windows per K0 pass (of3d_plan_execute_ahead)") if kb >= 2 else
+                                 ("frame pipelining (of3d_plan_execute_next)" if not args.no_pipeline else "plain")},
+            "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "build": build_stamp(),
         }
+        if split_detail is not None:
+            line["split"] = split_detail
+        if replicas is not None:
+            line["replicas"] = replicas
+        if other is not None:
+            line["row_slabs" if axis == 0 else "z_slabs"] = other
         print(json.dumps(line), flush=True)
-    sb.close()
 
 
 def build_stamp():
@@ -632,13 +797,36 @@ def build_stamp():
     return {"src_hash": i["src_hash"], "tree_hash": i["tree_hash"], "extra": i["extra"], "lib": i["lib"]}
 
 
-def parity_sample(d_in, outs, box, s, t, w, fp32=False):
-    """The headline run's outputs checked against the oracle (oracle/cpu_ref.py, the CPU
-    restatement pinned to the reference) on one crop — outside the timed region, the checker
-    only.  Output voxels further than rd + rw from every face where the crop cuts the volume
-    are exact (tests/test_gpu_bench_geometry.py); vx/vy/vz must match bit for bit (fp32
-    runs: within 1e-4 max|v|), rel within 1e-6 lambda_max."""
+def parity_check(sub, lo, box, got, s, t, w, fp32=False):
+    """Outputs `got` (vx, vy, vz, rel host arrays of the box) against the oracle
+    (oracle/cpu_ref.py, the CPU restatement pinned to the reference) run on `sub`, the
+    window's uint16 input over the box + the rd + rw halo (origin `lo`) — outside any timed
+    region, the checker only.  Output voxels further than rd + rw from every face where the
+    crop cuts the volume are exact (tests/test_gpu_bench_geometry.py): vx/vy/vz must match bit
+    for bit (fp32 runs: within 1e-4 max|v|), rel within 1e-6 lambda_max (fp32: 1e-4)."""
     from oracle import cpu_ref
+
+    z0, z1, y0, y1, x0, x1 = box
+    st = cpu_ref.structure_tensor3d(np.ascontiguousarray(sub), s, t, w, backend="scipy")
+    want = cpu_ref.solve3d(st)
+    lmin, lmax = cpu_ref.eig_fp64_3d(st)
+    sl = (slice(z0 - lo[0], z1 - lo[0]), slice(y0 - lo[1], y1 - lo[1]), slice(x0 - lo[2], x1 - lo[2]))
+    if fp32:
+        dv = max(float(np.abs(np.asarray(g, np.float64) - v[sl]).max() / np.abs(v[sl]).max())
+                 for g, v in zip(got, want))
+        ok_v = dv <= 1e-4
+    else:
+        ok_v = all(np.array_equal(np.ascontiguousarray(g, np.float64).view(np.uint64),
+                                  np.ascontiguousarray(v[sl]).view(np.uint64)) for g, v in zip(got, want))
+    rel_err = float(np.max(np.abs(np.asarray(got[3], np.float64) - lmin[sl]) / (np.abs(lmax[sl]) + 1e-300)))
+    ok = bool(ok_v and rel_err <= (1e-4 if fp32 else 1e-6))
+    return {"ok": ok, "crop_out": list(box), "vxyz": ("within 1e-4 max|v|" if fp32 else "bitwise") if ok_v else
+            "MISMATCH", "rel_max_err_over_lmax": rel_err, "checker": "oracle/cpu_ref.py (scipy backend)"}
+
+
+def parity_sample(d_in, outs, box, s, t, w, fp32=False):
+    """The single-GPU headline's parity sample: one crop of the resident outputs against the
+    oracle of the same device input (parity_check)."""
     from opticalflow3d_dev_amd import radii
 
     rd, _, _, rw = radii(s, t, w)
@@ -647,21 +835,9 @@ def parity_sample(d_in, outs, box, s, t, w, fp32=False):
     z0, z1, y0, y1, x0, x1 = box
     lo = [max(a - h, 0) for a in (z0, y0, x0)]
     hi = [min(b + h, n) for b, n in zip((z1, y1, x1), (nz, ny, nx))]
-    sub = np.ascontiguousarray(d_in[:, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]].cpu().numpy().view(np.uint16))
-    st = cpu_ref.structure_tensor3d(sub, s, t, w, backend="scipy")
-    want = cpu_ref.solve3d(st)
-    lmin, lmax = cpu_ref.eig_fp64_3d(st)
-    sl = (slice(z0 - lo[0], z1 - lo[0]), slice(y0 - lo[1], y1 - lo[1]), slice(x0 - lo[2], x1 - lo[2]))
+    sub = d_in[:, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]].cpu().numpy().view(np.uint16)
     got = [o.view(nz, ny, nx)[z0:z1, y0:y1, x0:x1].cpu().numpy() for o in outs]
-    if fp32:
-        dv = max(float(np.abs(g.astype(np.float64) - v[sl]).max() / np.abs(v[sl]).max()) for g, v in zip(got, want))
-        ok_v = dv <= 1e-4
-    else:
-        ok_v = all(np.array_equal(g.view(np.uint64), v[sl].view(np.uint64)) for g, v in zip(got, want))
-    rel_err = float(np.max(np.abs(got[3].astype(np.float64) - lmin[sl]) / (np.abs(lmax[sl]) + 1e-300)))
-    ok = bool(ok_v and rel_err <= (1e-4 if fp32 else 1e-6))
-    return {"ok": ok, "crop_out": list(box), "vxyz": ("within 1e-4 max|v|" if fp32 else "bitwise") if ok_v else
-            "MISMATCH", "rel_max_err_over_lmax": rel_err, "checker": "oracle/cpu_ref.py (scipy backend)"}
+    return parity_check(sub, lo, box, got, s, t, w, fp32)
 
 
 def main():
@@ -669,15 +845,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
-                    help="c3 = configs[2], the largest single-GPU config (the headline); c2 = configs[1]")
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c3 = configs[2] on one GPU (the single-GPU headline); at N > 1 the volume "
+                         "the BASELINE config names for N GPUs, z-sharded over the ranks: c4 = configs[3] "
+                         "(2 and 4 GPUs), c5 = configs[4] (8 GPUs); c2 = configs[1]")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--overlap", type=int, default=int(os.environ.get("OF3D_BENCH_OVERLAP", "-1")),
                     help="z chunk (output planes) of the plan's overlap mode; 0 = serial; -1 = the plan's default")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU work for cpu_baseline")
-    ap.add_argument("--split", default="auto", choices=("auto", "z", "y"),
-                    help="c4/c5: split axis of the volume over the ranks (auto: less halo work)")
-    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling split of the frame")
+    ap.add_argument("--split", default="z", choices=("auto", "z", "y"),
+                    help="c4/c5 and N > 1: split axis of the volume over the ranks (z: the north star's "
+                         "z-shard, the default; auto: the axis with less halo work, process_flow's choice)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the other axis's split (sub-object)")
+    ap.add_argument("--no-replicas", action="store_true",
+                    help="N > 1: skip the one-GPU frame of the same volume on every rank (t1 of the efficiency)")
+    ap.add_argument("--no-single-window", action="store_true",
+                    help="c2/c3: skip the single-window measurement (2rt+1 resident frames, K0 every step)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="neither K0 batching nor frame pipelining: every step launches its own K0 "
                          "(of3d_plan_execute)")
@@ -693,6 +876,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    explicit = args.config is not None
+    if not explicit:  # the BASELINE config for this GPU count
+        args.config = "c3" if world == 1 else ("c4" if world < 8 else "c5")
     nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
 
     import torch
@@ -712,7 +898,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    if args.config in ZSLAB_CONFIGS:
+    if args.config in ZSLAB_CONFIGS or (world > 1 and not explicit):
         run_slab(args, world, rank, local_rank, dev)
         if world > 1:
             dist.destroy_process_group()
@@ -773,8 +959,30 @@ def main():
     # sanity: finite outputs
     finite = bool(torch.isfinite(d_vx).all().item())
     kernels = set(plan.kernels())
-    plan.close()
     ms_step = elapsed / args.steps * 1e3
+    parity = None
+    if rank == 0 and not args.no_parity_sample:
+        # one 16^3 output crop across the kernels' seams (K5c / K12 z chunk 64, K34 row chunk
+        # 256 at c3) against the oracle, outside the timed region
+        zc, yc, xc = min(64, nz // 2), min(256, ny // 2), nx // 2 + 44
+        box = (zc - 8, zc + 8, yc - 8, yc + 8, min(xc, nx - 16), min(xc, nx - 16) + 16)
+        jl = last["j"]  # the window of the last step (its outputs are in d_v*)
+        parity = parity_sample(d_in[jl:jl + nwin], (d_vx, d_vy, d_vz, d_rel), box, s, t, w, fp32)
+    single = None
+    if kb and not args.no_single_window:
+        # configs[2] as stated: ONE window of 2rt+1 resident frames, every step a plain
+        # of3d_plan_execute (K0 every step), the same warmup / steps between barrier + sync
+        def step1():
+            plan.execute(fptrs, _lib.OF3D_U16, 0, 0, nz, d_vx.data_ptr(), d_vy.data_ptr(), d_vz.data_ptr(),
+                         d_rel.data_ptr(), stream)
+
+        el1 = timed_steps(step1, args.steps, args.warmup, world, dev)
+        single = {"ms_per_step": round(el1 / args.steps * 1e3, 5),
+                  "value": round(world * vox * args.steps / el1 / 1e6, 3), "unit": "Mvoxels/s",
+                  "resident_frames": nwin,
+                  "what": f"one {nwin}-frame window resident (configs[{int(args.config[1:]) - 1}] as stated), a plain "
+                          "of3d_plan_execute per step: K0 + K12 + K34 + K5c every step"}
+    plan.close()
 
     # N > 1: the same frame split over the ranks (strong scaling, halo exchange over RCCL):
     # z-slabs (the north star's axis) and the axis with less halo work (row slabs here)
@@ -789,7 +997,8 @@ def main():
                 continue
             try:  # the replica line stands on its own: a failed split is reported in it, not fatal
                 r = strong_split(args.config, ax, world, rank, dev, args.steps, args.warmup, ms_step,
-                                 pipeline=not args.no_pipeline, k0_batch=kb)
+                                 pipeline=not args.no_pipeline, k0_batch=kb, fp32=fp32,
+                                 parity=not args.no_parity_sample)
             except Exception as e:  # noqa: BLE001
                 r = {"error": f"{type(e).__name__}: {e}"[:300]}
             strong["zslab" if ax == 0 else "yslab"] = r
@@ -799,26 +1008,22 @@ def main():
         roof = roofline(profile, dom, dom_ms, stage_model(nwin, rd, rs, rt, rw, nz, nz, nz, ny * nx, sv),
                         args.config if not fp32 else args.config + "_fp32", (nwin * 2 + 3 * sv + 4) * vox,
                         frame_ops_per_voxel(rd, rs, rt, rw) * vox, nwin, sv, used=kernels)
-        cpu = parity = None
+        cpu = None
         if world == 1 and not args.no_cpu_baseline:
             sub = min(cpu_sample_planes(nz, ny, nx, args.cpu_budget), nz)
             host = d_in[:nwin, :sub].cpu().numpy().view(np.uint16)
             cpu = cpu_baseline(host, s, t, w, args.cpu_budget, nz_total=nz, cfg=args.config)
-        if not args.no_parity_sample:
-            # one 16^3 output crop across the kernels' seams (K5c / K12 z chunk 64, K34 row chunk
-            # 256 at c3) against the oracle, outside the timed region
-            zc, yc, xc = min(64, nz // 2), min(256, ny // 2), nx // 2 + 44
-            box = (zc - 8, zc + 8, yc - 8, yc + 8, min(xc, nx - 16), min(xc, nx - 16) + 16)
-            jl = last["j"]  # the window of the last step (its outputs are in d_v*)
-            parity = parity_sample(d_in[jl:jl + nwin], (d_vx, d_vy, d_vz, d_rel), box, s, t, w, fp32)
         line = {
             "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
             "value": round(value, 3), "unit": "Mvoxels/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32" if fp32 else "f64", "data": "synthetic",
-            "config": {"workload": desc, "nt": nt, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s, "tSig": t,
-                       "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
-                       "inputs": "2*rt+1 uint16 frames resident in HBM", "outputs_finite": finite,
+            "config": {"workload": desc, "nt": nres, "nt_window": nwin, "nz": nz, "ny": ny, "nx": nx, "xyzSig": s,
+                       "tSig": t, "wSig": w, "parallelism": f"frame replicas x{world}" if world > 1 else "single GPU",
+                       "inputs": (f"a time series of {nres} uint16 frames resident in HBM: {kb} consecutive "
+                                  f"{nwin}-frame windows (output frames), step i computes window i mod {kb}"
+                                  if kb else f"one {nwin}-frame window of uint16 frames resident in HBM"),
+                       "outputs_finite": finite,
                        "frame_pipelining": ("each step's W-z/solve kernel also forms the next step's temporal "
                                             "derivative (of3d_plan_execute_next); stage grad_xy is then empty")
                        if pipe else None,
@@ -831,6 +1036,10 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "parity_sample": parity, "build": build_stamp(),
         }
+        if single is not None:
+            line["single_window_ms"] = single["ms_per_step"]
+            line["single_window_value"] = single["value"]
+            line["single_window"] = single
         if strong is not None:
             line["strong"] = dict(strong, note="the same frame split over the ranks (halo exchange over "
                                                "RCCL P2P beside compute); value = frame voxels / step time")

@@ -919,8 +919,8 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             // planes per block: the longest march (up to 256) that still gives >= 1024 blocks
             // (each march re-forms 2 rd halo planes), at least 16.  Measured: c5 fp32 K12 20.7 /
             // 20.0 / 19.7 ms at 64 / 128 / 256, c4 fp64 4.40 / 4.12 at 64 / 128; c3 keeps 64
-            static const int zc_env = getenv("OF3D_K12_ZC") ? atoi(getenv("OF3D_K12_ZC")) : 0;
-            int zc = zc_env;
+            const char* zc_env = getenv("OF3D_K12_ZC");  // forced march length (tests, experiments)
+            int zc = zc_env ? atoi(zc_env) : 0;
             if (zc <= 0) {
                 zc = 256;
                 while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;

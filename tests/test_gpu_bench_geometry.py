@@ -216,3 +216,85 @@ def test_more_than_64_planes_small_xy_vs_oracle(variant):
     for g, want, name in zip(outs[:3], (vx, vy, vz), ("vx", "vy", "vz")):
         assert bits_equal(g.cpu().numpy(), want), (variant, name, kernels)
     assert_rel_within(outs[3].cpu().numpy(), lmin, lmax, 1e-6)
+
+
+# ---- configs[3] / configs[4] geometry (round 4): the branches only the big volumes take ----
+
+LONG = dict(nt=13, nz=320, ny=40, nx=48, s=2, t=2, w=5)
+
+
+@pytest.fixture(scope="module")
+def long_volume():
+    """A >= 300-plane small-xy volume (13 x 320 x 40 x 48, sigma 2, tau 2, omega 5) and its
+    full oracle: K12's 128- and 256-plane z marches (what c4 / c5 run: csrc/of3d_host.hip picks
+    the longest march that still gives >= 1024 blocks) have whole marches and a tail here."""
+    import torch
+
+    p = LONG
+    img = np.random.default_rng(320).integers(0, 4096, size=(p["nt"], p["nz"], p["ny"], p["nx"])).astype(np.uint16)
+    d_in = torch.from_numpy(np.ascontiguousarray(img).view(np.int16)).to("cuda")
+    yield d_in, oracle3d(img, p["s"], p["t"], p["w"])
+    del d_in
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+@pytest.mark.parametrize("zc", [128, 256])
+def test_k12_long_marches_vs_oracle(long_volume, zc, fp32):
+    """OF3D_K12_ZC = 128 / 256 (the c4 / c5 marches) against the full oracle: fp64 bitwise,
+    fp32 within 1e-4 max|v| and bit-identical to the 16-plane marches of the same plan."""
+    from opticalflow3d_dev_amd import _lib
+
+    d_in, (vx, vy, vz, lmin, lmax) = long_volume
+    p = LONG
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    with env(OF3D_K12=1, OF3D_K12_ZC=zc):
+        outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+    assert "k_grad_xyz_c" in kernels, kernels
+    if not fp32:
+        for g, want, name in zip(outs[:3], (vx, vy, vz), ("vx", "vy", "vz")):
+            assert bits_equal(g.cpu().numpy(), want), (zc, name)
+        assert_rel_within(outs[3].cpu().numpy(), lmin, lmax, 1e-6)
+        return
+    for g, want in zip(outs[:3], (vx, vy, vz)):
+        assert np.abs(g.cpu().numpy().astype(np.float64) - want).max() <= 1e-4 * np.abs(want).max()
+    with env(OF3D_K12=1, OF3D_K12_ZC=16):
+        short, _ = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+    for a, b, name in zip(outs, short, ("vx", "vy", "vz", "rel")):
+        assert same_bits(a, b), (zc, name)
+
+
+C5S = dict(nt=13, nz=48, ny=64, nx=2048, s=2, t=2, w=5)
+
+
+def test_c5_shaped_fp32_plan_candidates_and_oracle():
+    """configs[4]'s row geometry (nx = 2048, rw 15, fp32: the packed K34 with its 2048-wide
+    rows, K34's whole-column row chunks grouped per plane, K12's 256-plane march) on a thin
+    slab of c5's own synthetic family: every K34 autotune candidate bit-identical, and oracle
+    crops (interior and the far corner) within 1e-4 of the fp64 oracle."""
+    import torch
+
+    import bench
+    from opticalflow3d_dev_amd import _lib
+
+    p = C5S
+    dev = torch.device("cuda", 0)
+    d_in = bench.synthetic_slab(p["nt"], p["nz"], p["ny"], p["nx"], 0, p["nz"], 20260206 + 5, dev)
+    host_in = d_in.cpu().numpy().view(np.uint16)
+    mode = _lib.OF3D_FP32
+    with env(OF3D_K12=1, OF3D_K12_ZC=256):
+        ref, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+        assert "k_grad_xyz_c" in kernels, kernels
+        ncand = k34_candidates(d_in, p, mode)
+        assert ncand >= 2
+        seen = set(kernels)
+        for i in range(ncand):
+            with env(OF3D_K34_CAND=i):
+                outs, ks = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+            seen.update(ks)
+            for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
+                assert same_bits(a, b), (i, name, ks)
+            del outs
+    assert "k_prod_wyx_pk" in seen, seen
+    crop_check(host_in, ref, (16, 32, 24, 40, 1016, 1040), p["s"], p["t"], p["w"], fp32=True)
+    crop_check(host_in, ref, (32, 48, 44, 64, 2020, 2048), p["s"], p["t"], p["w"], fp32=True)
