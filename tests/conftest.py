@@ -17,10 +17,15 @@ def pytest_configure(config):
 
 
 def _gpu_count():
+    """Devices the HIP library sees; 0 without a GPU.  On a machine WITH a GPU (/dev/kfd) a
+    library that does not load (missing, stale sources, wrong arch) is an error, never a skip:
+    the GPU tests must run through libof3d.so or fail."""
     try:
         from opticalflow3d_dev_amd import _lib
         return _lib.load().of3d_device_count()
-    except Exception:
+    except Exception as e:
+        if os.path.exists("/dev/kfd"):
+            raise pytest.UsageError(f"GPU present but libof3d.so does not load: {e}") from e
         return 0
 
 
