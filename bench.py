@@ -531,6 +531,27 @@ def timed_steps(step, steps, warmup, world, dev):
     return max_over_ranks([el], dev)[0] if world > 1 else el
 
 
+def gather_owned_crop(crop, rank, world, dev):
+    """Every rank's (5, ...) crop — 4 outputs + an ownership mask of its own voxels — merged on
+    rank 0 (all_gather over the process group: device tensors on RCCL, host tensors on gloo):
+    the sum of the owned values and the count of owners per voxel (1 everywhere when the slabs
+    tile the crop).  Rank 0 gets the merged crop, the others None."""
+    import torch
+    import torch.distributed as dist
+
+    where = dev if dist.get_backend() == "nccl" else "cpu"
+    mine = crop.to(where)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine)
+    if rank != 0:
+        return None
+    out = torch.zeros_like(mine)
+    for q in parts:
+        out[:4] += q[:4] * q[4]
+        out[4] += q[4]
+    return out
+
+
 def slab_parity(sb, fp32):
     """parity_sample of a slab run (every rank calls it; rank 0 returns the result, the others
     None): one 16^3 output crop straddling the cut between rank 0 and rank 1 on the split axis
@@ -548,12 +569,7 @@ def slab_parity(sb, fp32):
     world = 1 if sb.vrank else sb.world
     n_ax = dims[sb.axis]
     cut = zslab_bounds(n_ax, 0, world)[1] if world > 1 else n_ax // 2
-    ctr = [nz // 2, ny // 2, nx // 2 + 44]
-    ctr[sb.axis] = cut
-    box = []
-    for c, n in zip(ctr, dims):
-        a = min(max(c - 8, 0), max(n - 16, 0))
-        box += [a, min(a + 16, n)]
+    box = list(parity_box(dims, sb.axis, cut))
     z0, z1, y0, y1, x0, x1 = box
     # this rank's own outputs inside the box: 4 outputs + an ownership mask, as float64
     crop = torch.zeros((5, z1 - z0, y1 - y0, x1 - x0), dtype=torch.float64, device=sb.dev)
@@ -574,16 +590,9 @@ def slab_parity(sb, fp32):
         else:
             crop[4, :, o0 - y0:o1 - y0] = 1
     if world > 1:
-        where = sb.dev if dist.get_backend() == "nccl" else "cpu"
-        mine = crop.to(where)
-        parts = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(parts, mine)
-        if sb.rank != 0:
+        crop = gather_owned_crop(crop, sb.rank, world, sb.dev)
+        if crop is None:
             return None
-        crop = torch.zeros_like(mine)
-        for q in parts:
-            crop[:4] += q[:4] * q[4]
-            crop[4] += q[4]
     if not bool((crop[4] == 1).all()):
         return {"ok": False, "error": "crop voxels not owned exactly once", "crop_out": box}
     got = [crop[k].cpu().numpy() for k in range(4)]
@@ -597,6 +606,25 @@ def slab_parity(sb, fp32):
     r["where"] = ("across the cut between rank 0 and rank 1 (%s %d)" % ("plane" if sb.axis == 0 else "row", cut)
                   if world > 1 else "volume centre")
     return r
+
+
+def default_config(world):
+    """The BASELINE.json config named for `world` GPUs: configs[2] (c3) on one GPU, configs[3]
+    (c4, "z-slab split across 2 and 4 MI355X") below 8, configs[4] (c5, "8 MI355X") at 8+."""
+    return "c3" if world == 1 else ("c4" if world < 8 else "c5")
+
+
+def parity_box(dims, axis, cut, size=16, dx=44):
+    """The slab parity crop (z0, z1, y0, y1, x0, x1): `size` voxels per side centred on `cut`
+    along the split axis (the first rank cut; the volume centre on one GPU) and near the volume
+    centre (x offset dx) on the other axes, clipped into the volume."""
+    ctr = [dims[0] // 2, dims[1] // 2, dims[2] // 2 + dx]
+    ctr[axis] = cut
+    box = []
+    for c, n in zip(ctr, dims):
+        a = min(max(c - size // 2, 0), max(n - size, 0))
+        box += [a, min(a + size, n)]
+    return tuple(box)
 
 
 def slab_on_every_rank(world, dev, *a, **kw):
@@ -878,7 +906,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     explicit = args.config is not None
     if not explicit:  # the BASELINE config for this GPU count
-        args.config = "c3" if world == 1 else ("c4" if world < 8 else "c5")
+        args.config = default_config(world)
     nt, nz, ny, nx, s, t, w, desc = CONFIGS[args.config]
 
     import torch

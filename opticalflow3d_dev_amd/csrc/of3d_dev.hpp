@@ -721,6 +721,44 @@ __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict
 // gradient rows that 9 products x column blocks read come from one L2.
 // ---------------------------------------------------------------------------
 constexpr int k34_nr(int rw, int s) { return ((2 * rw + 2 + s - 1) / s) * s; }
+// K34 block -> (plane zl, row chunk yc, column block bx, product p).  The linear workgroup id
+// b runs on XCD b % 8 (round-robin dispatch), so blocks that should share an L2 share b % 8.
+//   cpg > 0 (plane-major, the default): group g = (plane, run of cpg row chunks) =
+//     (b / 8 / mb) * 8 + b % 8, members (chunk in the run, product, column block); ngroups = groups.
+//   cpg < 0 (chunk-major, OF3D_K34_CM): XCD x runs planes x, x + 8, ..., each plane's row
+//     chunks one after another, every chunk's NP x nbx blocks dispatched together — the rows in
+//     flight on an XCD are one chunk's (and its 2 RW halo rows, the previous chunk's last rows);
+//     ngroups = planes.
+struct K34Blk {
+    int zl, yc, bx, p;
+    bool ok;
+};
+template <int NP>
+__device__ __forceinline__ K34Blk k34_block(int nbx, int nyb, int cpg, int ngroups) {
+    const int kb = blockIdx.x >> 3, xcd = blockIdx.x & 7;
+    K34Blk r;
+    if (cpg < 0) {
+        const int mb = NP * nbx, k = kb / mb, m = kb % mb;
+        r.bx = m % nbx;
+        r.p = m / nbx;
+        r.zl = xcd + 8 * (k / nyb);
+        r.yc = k % nyb;
+        r.ok = r.zl < ngroups;
+        return r;
+    }
+    const int mb = cpg * NP * nbx;
+    const int g = (kb / mb) * 8 + xcd;
+    int m = kb % mb;
+    r.bx = m % nbx;
+    m /= nbx;
+    r.p = m % NP;
+    const int ycl = m / NP, nyg = (nyb + cpg - 1) / cpg;
+    r.zl = g / nyg;
+    r.yc = (g % nyg) * cpg + ycl;
+    r.ok = g < ngroups && r.yc < nyb;
+    return r;
+}
+
 // W-y tile row r starts at r cwp + 28 (r / 4): with cwp = 1 (mod 32) every row start is
 // r mod 4 (mod 32) elements (bank-conflict-free phase B, see k_prod_wyx)
 __host__ __device__ constexpr int k34_row(int r, int cwp) { return r * cwp + 28 * (r / 4); }
@@ -824,17 +862,9 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const int t = threadIdx.x;
     // XCD-aware block decode: group g = (plane, run of cpg row chunks), member m = (chunk in the
     // run, product, column block): one group's blocks share an XCD and are dispatched together
-    const int mb = cpg * NP * nbx;
-    const int kb = blockIdx.x >> 3;
-    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
-    if (g >= ngroups) return;
-    int m = kb % mb;
-    const int bx = m % nbx;
-    m /= nbx;
-    const int p = m % NP, ycl = m / NP;
-    const int nyg = (nyb + cpg - 1) / cpg;
-    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
-    if (yc >= nyb) return;
+    const K34Blk kbk = k34_block<NP>(nbx, nyb, cpg, ngroups);
+    if (!kbk.ok) return;
+    const int bx = kbk.bx, p = kbk.p, zl = kbk.zl, yc = kbk.yc;
     // output rows [yb0, yb1) (row-slab plans: the rank's own rows; loads still clamp at [0, ny))
     const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
     const int xo0 = bx * tx;
@@ -1023,17 +1053,9 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
     F* sw = reinterpret_cast<F*>(smem_raw);  // two W-y tiles [2][S][cwp]
     const int cwp = k34_pitch(min(tx, nx), RW);
     const int t = threadIdx.x;
-    const int mb = cpg * NP * nbx;
-    const int kb = blockIdx.x >> 3;
-    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
-    if (g >= ngroups) return;
-    int m = kb % mb;
-    const int bx = m % nbx;
-    m /= nbx;
-    const int p = m % NP, ycl = m / NP;
-    const int nyg = (nyb + cpg - 1) / cpg;
-    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
-    if (yc >= nyb) return;
+    const K34Blk kbk = k34_block<NP>(nbx, nyb, cpg, ngroups);
+    if (!kbk.ok) return;
+    const int bx = kbk.bx, p = kbk.p, zl = kbk.zl, yc = kbk.yc;
     // output rows [yb0, yb1) (row-slab plans: the rank's own rows; loads still clamp at [0, ny))
     const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
     const int xo0 = bx * tx;
@@ -1200,17 +1222,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int P2 = k34_pitch(min(tx, nx), RW);
     const int TB = (S / 2) * P2;  // float2 per tile buffer
     const int t = threadIdx.x;
-    const int mb = cpg * NP * nbx;
-    const int kb = blockIdx.x >> 3;
-    const int g = (kb / mb) * 8 + (blockIdx.x & 7);
-    if (g >= ngroups) return;
-    int m = kb % mb;
-    const int bx = m % nbx;
-    m /= nbx;
-    const int p = m % NP, ycl = m / NP;
-    const int nyg = (nyb + cpg - 1) / cpg;
-    const int zl = g / nyg, yc = (g % nyg) * cpg + ycl;
-    if (yc >= nyb) return;
+    const K34Blk kbk = k34_block<NP>(nbx, nyb, cpg, ngroups);
+    if (!kbk.ok) return;
+    const int bx = kbk.bx, p = kbk.p, zl = kbk.zl, yc = kbk.yc;
     const int y0 = yb0 + yc * nyc, nrows = min(nyc, yb1 - y0);
     const int xo0 = bx * tx;
     const int txu = min(tx, nx - xo0);

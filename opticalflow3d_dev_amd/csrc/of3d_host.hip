@@ -402,7 +402,27 @@ template <typename K, typename F>
 hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
                       hipStream_t s, int yb0 = 0, int yb1 = -1) {
     if (yb1 < 0) yb1 = ny;
-    const int nyo = yb1 - yb0;  // output rows (row-slab plans: the own rows)
+    const int nyo = yb1 - yb0;  // output rows (row-slab plans: the rank's own rows)
+    int tx = k.tx, nbx = k.nbx;
+    // chunk-major order (k34_block, cpg < 0): the 9 products of a row chunk read the same four
+    // gradient rows, which stay in an XCD's L2 only while the chunk's blocks run together — c5's
+    // 79 GB of K34 reads per launch for 34 GB of gradients (planes of 32 MiB of gradient rows).
+    // Off by default: chunks of OF3D_K34_CM rows measured slower (c3 1.63 -> 1.66 / 1.71 / 1.85
+    // ms at 256 / 128 / 64 rows, c5 fp32 46.0 -> 48.5 / 50.3 ms at 128 / 64, c4 11.58 -> 11.37 /
+    // 11.59 / 11.82 at 256 / 128 / 64; profiles/r04/ab_k34_cm.txt): the re-formed halo rows of
+    // every chunk cost more than the L2 misses, which K34 (VALU-bound) mostly hides.
+    const char* ecm = getenv("OF3D_K34_CM");
+    const int cm_rows = ecm ? atoi(ecm) : 0;
+    if (cm_rows > 0 && nyo >= 2 * cm_rows) {
+        int nyc = (cm_rows + k.s - 1) / k.s * k.s;
+        const int nyb = (nyo + nyc - 1) / nyc;
+        int cpg = -1, groups = ng;
+        const int mb = nf * nbx;
+        const unsigned blocks = (unsigned)(8 * ((ng + 7) / 8) * nyb * mb);
+        void* args[] = {(void*)&G,   (void*)&P,   (void*)&ny,  (void*)&nx,  (void*)&fs,     (void*)&hw,  (void*)&tx,
+                        (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1};
+        return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);
+    }
     const int nyb_max = std::max(1, nyo / 32);
     // block target 2048: longer row chunks re-read fewer halo rows (c3 wave-specialised K34 1.67
     // vs 1.76 ms at 4096, 1.73 at 1024; c2 lockstep K34 0.175 vs 0.191 ms, frame 0.420 vs 0.435;
@@ -418,7 +438,6 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     int groups = ng * ((nyb + cpg - 1) / cpg);
     const int mb = cpg * nf * k.nbx;
     const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
-    int tx = k.tx, nbx = k.nbx;
     void* args[] = {(void*)&G,   (void*)&P,   (void*)&ny,  (void*)&nx,  (void*)&fs,     (void*)&hw,  (void*)&tx,
                     (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1};
     return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);

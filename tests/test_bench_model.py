@@ -55,3 +55,28 @@ def test_fused_solve_roofline_adds_k0(sv):
             == plain["kernel_hbm"]["workspace_bytes_per_launch"] + k0["bytes"])
     # the model dict the caller holds is not modified
     assert model["wz_solve"]["ops"] == plain["algorithmic_ops_per_launch"]
+
+
+def test_default_config_per_gpu_count():
+    """--gpus N without --config runs the volume BASELINE.json names for N GPUs."""
+    assert bench.default_config(1) == "c3"
+    assert bench.default_config(2) == "c4" and bench.default_config(4) == "c4"
+    assert bench.default_config(8) == "c5"
+    assert bench.CONFIGS["c4"][:4] == (13, 256, 1024, 1024) and bench.CONFIGS["c5"][:4] == (13, 512, 2048, 2048)
+
+
+@pytest.mark.parametrize("cfg,world,axis", [("c4", 2, 0), ("c4", 4, 0), ("c5", 8, 0), ("c4", 2, 1), ("c5", 8, 1),
+                                            ("c3", 1, 0)])
+def test_parity_box_straddles_the_first_cut(cfg, world, axis):
+    """The slab parity crop holds planes (rows) of rank 0 AND rank 1 — both sides of the first
+    cut — and lies inside the volume."""
+    from opticalflow3d_dev_amd.shard import zslab_bounds
+
+    nt, nz, ny, nx = bench.CONFIGS[cfg][:4]
+    dims = (nz, ny, nx)
+    cut = zslab_bounds(dims[axis], 0, world)[1] if world > 1 else dims[axis] // 2
+    box = bench.parity_box(dims, axis, cut)
+    for d in range(3):
+        assert 0 <= box[2 * d] < box[2 * d + 1] <= dims[d] and box[2 * d + 1] - box[2 * d] == 16
+    lo, hi = box[2 * axis], box[2 * axis + 1]
+    assert lo < cut < hi

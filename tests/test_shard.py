@@ -102,3 +102,59 @@ def test_halo_transfers_symmetric(nz, world, halo):
     got = sorted((r, p, a, b) for r in range(world) for p, a, b in sends[r])
     want = sorted((p, r, a, b) for r in range(world) for p, a, b in recvs[r])
     assert got == want
+
+
+def _crop_worker(rank, world, port, axis, q):
+    """bench.gather_owned_crop as slab_parity runs it: every rank fills the crop voxels of its
+    own planes (rows) of a known field; rank 0's merge must equal the field with every voxel
+    owned exactly once."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dims = (40, 36, 30)
+        n_ax = dims[axis]
+        cut = zslab_bounds(n_ax, 0, world)[1]
+        box = bench.parity_box(dims, axis, cut)
+        z0, z1, y0, y1, x0, x1 = box
+        field = torch.arange(40 * 36 * 30, dtype=torch.float64).reshape(dims)
+        want = field[z0:z1, y0:y1, x0:x1]
+        a0, a1 = zslab_bounds(n_ax, rank, world)
+        crop = torch.zeros((5,) + tuple(want.shape), dtype=torch.float64)
+        b0, b1 = box[2 * axis], box[2 * axis + 1]
+        o0, o1 = max(b0, a0), min(b1, a1)
+        if o1 > o0:
+            sl = [slice(None)] * 3
+            sl[axis] = slice(o0 - b0, o1 - b0)
+            for k in range(4):
+                crop[(k, *sl)] = want[tuple(sl)] * (k + 1)
+            crop[(4, *sl)] = 1
+        out = bench.gather_owned_crop(crop, rank, world, "cpu")
+        if rank == 0:
+            ok = bool((out[4] == 1).all()) and all(torch.equal(out[k], want * (k + 1)) for k in range(4))
+        else:
+            ok = out is None
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,axis", [(2, 0), (2, 1), (4, 0), (3, 1)])
+def test_bench_parity_crop_gather_gloo(world, axis):
+    """The N > 1 bench line's parity crop: straddles the rank-0/1 cut and is reassembled on
+    rank 0 from its owners (gloo, CPU)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_crop_worker, args=(r, world, port, axis, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res

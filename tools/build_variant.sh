@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build an A/B variant of libof3d.so from the current sources with extra compile flags:
+#   tools/build_variant.sh NAME "-DMACRO=0 ..."   ->  tools/variants/NAME.so
+# (a copy of csrc/ + include/ under /tmp, so the tree's own objects stay untouched)
+set -eu
+REPO=$(cd "$(dirname "$0")/.." && pwd)
+NAME=$1; FLAGS=${2:-}
+D=/tmp/of3d_variant_$NAME
+rm -rf "$D"; mkdir -p "$D/opticalflow3d_dev_amd" "$REPO/tools/variants"
+cp -r "$REPO/include" "$D/include"
+cp -r "$REPO/opticalflow3d_dev_amd/csrc" "$D/opticalflow3d_dev_amd/csrc"
+rm -rf "$D/opticalflow3d_dev_amd/csrc/build"
+make -C "$D/opticalflow3d_dev_amd/csrc" -j8 OUT="$REPO/tools/variants/$NAME.so" EXTRA="$FLAGS" > "$D/build.log" 2>&1 \
+  || { tail -20 "$D/build.log"; exit 1; }
+echo "built tools/variants/$NAME.so ($FLAGS)"
