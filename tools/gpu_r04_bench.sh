@@ -12,6 +12,15 @@ for c in ${CFGS:-c3 c2 c4 c5}; do
   rc=$?; echo "bench $c rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/${TAG}_${c}_bench.log | head -1) $(grep -o '"parity_sample": {"ok": [a-z]*' $OUT/${TAG}_${c}_bench.log)"
   [ $rc -eq 0 ] || { tail -5 $OUT/${TAG}_${c}_bench.log; exit $rc; }
 done
+# per-rank compute of the N > 1 z-slab splits on this one GPU (OF3D_BENCH_VRANK="r/P": rank r of a
+# P-way split alone, no exchange): what the driver's 2 / 4 / 8-GPU lines run per rank
+for v in ${VRANKS:-}; do
+  IFS=: read c rp <<< "$v"
+  OF3D_BENCH_VRANK=$rp timeout -k 10 420 python bench.py --config $c --split z --steps 20 --warmup 5 --no-cpu-baseline \
+    > $OUT/${TAG}_${c}_vrank_${rp/\//of}.log 2>&1
+  rc=$?; echo "vrank $c $rp rc=$rc $(grep -o '"ms_per_step": [0-9.]*' $OUT/${TAG}_${c}_vrank_${rp/\//of}.log | head -1)"
+  [ $rc -eq 0 ] || { tail -5 $OUT/${TAG}_${c}_vrank_${rp/\//of}.log; exit $rc; }
+done
 export TMPDIR=/tmp
 cd /tmp
 for c in ${PROF_CFGS:-c3 c5}; do
