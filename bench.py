@@ -430,6 +430,11 @@ class SlabBench:
         self.rel = torch.empty(max(n_out, 1), dtype=torch.float32, device=dev)
         self.comp = torch.cuda.current_stream(dev)
         self.xs = torch.cuda.Stream(device=dev)
+        # the ring was generated on the compute stream: the first exchanges (on xs, before any
+        # compute event exists for their slots) must not send or overwrite planes still being
+        # generated — the 4-rank gloo rehearsal caught halo planes received before the
+        # sender's generation finished (a slot exchanged only once before the parity window)
+        self.xs.wait_stream(self.comp)
         self.done = {}  # slot -> event of the last compute that read it
         self.xev = {}   # slot -> event of its frame's halo exchange (not yet waited for)
         self.order = list(range(self.nwin + self.L))  # the window (+ the lookahead frames)
@@ -534,8 +539,8 @@ def timed_steps(step, steps, warmup, world, dev):
 def gather_owned_crop(crop, rank, world, dev):
     """Every rank's (5, ...) crop — 4 outputs + an ownership mask of its own voxels — merged on
     rank 0 (all_gather over the process group: device tensors on RCCL, host tensors on gloo):
-    the sum of the owned values and the count of owners per voxel (1 everywhere when the slabs
-    tile the crop).  Rank 0 gets the merged crop, the others None."""
+    each voxel's value from its owner (bits kept) and the count of owners per voxel (1
+    everywhere when the slabs tile the crop).  Rank 0 gets the merged crop, the others None."""
     import torch
     import torch.distributed as dist
 
@@ -546,10 +551,48 @@ def gather_owned_crop(crop, rank, world, dev):
     if rank != 0:
         return None
     out = torch.zeros_like(mine)
-    for q in parts:
-        out[:4] += q[:4] * q[4]
+    for q in parts:  # select, not sum: keeps the owner's bits (-0.0 included)
+        own = q[4] > 0
+        out[:4] = torch.where(own, q[:4], out[:4])
         out[4] += q[4]
     return out
+
+
+def ring_check(sb, lo, hi):
+    """Diagnostics of a failed slab parity sample (rank 0's own ring): for each frame of the last
+    window, the planes (rows) of the crop's input box that rank 0 holds, compared with their
+    regeneration from the synthetic family — which input frames, if any, differ."""
+    import torch
+
+    nz, ny, nx = sb.dims
+    out = {}
+    a0, a1 = (lo[0], hi[0]) if sb.axis == 0 else (lo[1], hi[1])
+    b0, b1 = max(a0, sb.ai0), min(a1, sb.ai1)
+    if b1 <= b0:
+        return {"note": "rank 0 holds none of the box"}
+    for pos, sl in enumerate(sb.last_window):
+        if sb.axis == 0:
+            have = sb.ring[sl][b0 - sb.ai0:b1 - sb.ai0, lo[1]:hi[1], lo[2]:hi[2]]
+            want = synthetic_slab(1, nz, ny, nx, b0, b1, sb.seed + sl, sb.dev, rows=(lo[1], hi[1]))[0][:, :, lo[2]:hi[2]]
+        else:
+            have = sb.ring[sl][lo[0]:hi[0], b0 - sb.ai0:b1 - sb.ai0, lo[2]:hi[2]]
+            want = synthetic_slab(1, nz, ny, nx, lo[0], hi[0], sb.seed + sl, sb.dev, rows=(b0, b1))[0][:, :, lo[2]:hi[2]]
+        bad = (have != want)
+        if bool(bad.any()):
+            idx = bad.nonzero()
+            planes = sorted(set(int(v) for v in idx[:, 0].tolist()))
+            rec = {"n": int(bad.sum()), "planes_abs": [b0 + v for v in planes][:24]}
+            # whose frame is it?  the seed (ring slot) whose regeneration matches the first bad plane
+            q = planes[0]
+            for other in range(len(sb.ring)):
+                if sb.axis == 0:
+                    w2 = synthetic_slab(1, nz, ny, nx, b0 + q, b0 + q + 1, sb.seed + other, sb.dev,
+                                        rows=(lo[1], hi[1]))[0][:, :, lo[2]:hi[2]]
+                    if bool(torch.equal(have[q:q + 1], w2)):
+                        rec["first_bad_plane_is_slot"] = other
+                        break
+            out[f"pos{pos}_slot{sl}"] = rec
+    return out or {"note": "rank 0's input planes of the box equal their regeneration", "window": sb.last_window}
 
 
 def slab_parity(sb, fp32):
@@ -603,6 +646,9 @@ def slab_parity(sb, fp32):
     sub = np.stack([synthetic_slab(1, nz, ny, nx, lo[0], hi[0], sb.seed + sl, sb.dev, rows=(lo[1], hi[1]))[0]
                     [:, :, lo[2]:hi[2]].cpu().numpy().view(np.uint16) for sl in sb.last_window])
     r = parity_check(sub, lo, box, got, *sb.sig, fp32=fp32)
+    if not r["ok"] and os.environ.get("OF3D_BENCH_RING_CHECK", "1") == "1":
+        r["ring_check"] = ring_check(sb, lo, hi)
+    r["window_slots"] = list(sb.last_window)
     r["where"] = ("across the cut between rank 0 and rank 1 (%s %d)" % ("plane" if sb.axis == 0 else "row", cut)
                   if world > 1 else "volume centre")
     return r
@@ -848,8 +894,16 @@ def parity_check(sub, lo, box, got, s, t, w, fp32=False):
                                   np.ascontiguousarray(v[sl]).view(np.uint64)) for g, v in zip(got, want))
     rel_err = float(np.max(np.abs(np.asarray(got[3], np.float64) - lmin[sl]) / (np.abs(lmax[sl]) + 1e-300)))
     ok = bool(ok_v and rel_err <= (1e-4 if fp32 else 1e-6))
-    return {"ok": ok, "crop_out": list(box), "vxyz": ("within 1e-4 max|v|" if fp32 else "bitwise") if ok_v else
-            "MISMATCH", "rel_max_err_over_lmax": rel_err, "checker": "oracle/cpu_ref.py (scipy backend)"}
+    r = {"ok": ok, "crop_out": list(box), "vxyz": ("within 1e-4 max|v|" if fp32 else "bitwise") if ok_v else
+         "MISMATCH", "rel_max_err_over_lmax": rel_err, "checker": "oracle/cpu_ref.py (scipy backend)"}
+    if not ok_v:  # where and how far (crop-relative z planes of the differing voxels)
+        diff = [np.asarray(g, np.float64) != v[sl] for g, v in zip(got[:3], want)]
+        bad = diff[0] | diff[1] | diff[2]
+        r["n_mismatch"] = int(bad.sum())
+        r["mismatch_planes"] = sorted(set(int(z) for z in np.nonzero(bad)[0]))
+        r["max_abs_diff_over_max"] = max(float(np.abs(np.asarray(g, np.float64) - v[sl]).max() /
+                                             (np.abs(v[sl]).max() + 1e-300)) for g, v in zip(got[:3], want))
+    return r
 
 
 def parity_sample(d_in, outs, box, s, t, w, fp32=False):

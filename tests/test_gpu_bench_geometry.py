@@ -318,3 +318,36 @@ def test_k34_chunk_major_order_bit_identical(long_volume, mode, cm):
             outs, ks = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=m)
         for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
             assert same_bits(a, b), (cm, i, name, ks)
+
+
+C4S = dict(nt=13, nz=24, ny=64, nx=1024, s=2, t=2, w=5)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_c4_shaped_plan_every_k34_candidate(fp32):
+    """configs[3]'s row geometry (nx = 1024, rw 15: the K34 autotune's column-block shapes for a
+    1024-wide row) on a thin slab of c4's synthetic family: every K34 candidate bit-identical to
+    the default plan (the timing-based autotune may pick any of them on the driver's nodes), and
+    oracle crops across the candidates' column-block seams and at both x edges."""
+    import torch
+
+    import bench
+    from opticalflow3d_dev_amd import _lib
+
+    p = C4S
+    dev = torch.device("cuda", 0)
+    d_in = bench.synthetic_slab(p["nt"], p["nz"], p["ny"], p["nx"], 0, p["nz"], 20260206 + 4, dev)
+    host_in = d_in.cpu().numpy().view(np.uint16)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    ref, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+    ncand = k34_candidates(d_in, p, mode)
+    assert ncand >= 2
+    for i in range(ncand):
+        with env(OF3D_K34_CAND=i):
+            outs, ks = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+        for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
+            assert same_bits(a, b), (i, name, ks)
+        del outs
+    for box in ((4, 20, 24, 40, 330, 360), (4, 20, 24, 40, 500, 530), (4, 20, 24, 40, 676, 700),
+                (4, 20, 40, 64, 0, 24), (0, 16, 0, 20, 1000, 1024)):
+        crop_check(host_in, ref, box, p["s"], p["t"], p["w"], fp32=fp32)

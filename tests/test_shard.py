@@ -123,6 +123,7 @@ def _crop_worker(rank, world, port, axis, q):
         box = bench.parity_box(dims, axis, cut)
         z0, z1, y0, y1, x0, x1 = box
         field = torch.arange(40 * 36 * 30, dtype=torch.float64).reshape(dims)
+        field[::3] = -0.0  # owners' -0.0 bits survive the merge
         want = field[z0:z1, y0:y1, x0:x1]
         a0, a1 = zslab_bounds(n_ax, rank, world)
         crop = torch.zeros((5,) + tuple(want.shape), dtype=torch.float64)
@@ -136,7 +137,8 @@ def _crop_worker(rank, world, port, axis, q):
             crop[(4, *sl)] = 1
         out = bench.gather_owned_crop(crop, rank, world, "cpu")
         if rank == 0:
-            ok = bool((out[4] == 1).all()) and all(torch.equal(out[k], want * (k + 1)) for k in range(4))
+            ok = bool((out[4] == 1).all()) and all(
+                torch.equal(out[k].view(torch.int64), (want * (k + 1)).view(torch.int64)) for k in range(4))
         else:
             ok = out is None
         q.put((rank, ok))
