@@ -212,3 +212,23 @@ def test_process_flow_fp32_vs_oracle(tmp_path, fileType):
         assert_fp32_flow_close(got, stack[hh:hh + 7], 1, 1, 2)
         for g, d in zip(got, calc_flow3D_fp32(stack[hh:hh + 7], 1, 1, 2)):
             assert bits_equal(g, d)  # the ring path = the one-shot fp32 entry, bit for bit
+
+
+@pytest.mark.parametrize("name", ["c3d_ramp_xy_planar", "c3d_wave_planar", "c3d_ramp_xyz_rank1"])
+def test_matlab_output_near_degenerate(tmp_path, name):
+    """MATLAB mode end to end (M/calc_flow3D.m:235-236's double pageeig) on the near-degenerate
+    golden inputs — where the trigonometric eigenvalue alone misses 1e-10 lambda_max: the rel
+    file is within 1e-10 lambda_max of the fixture's fp64 eigvalsh, vx bit-identical to the
+    reference's."""
+    from conftest import load_golden
+
+    g = load_golden(name)
+    stack = g["images"]
+    tf.imwrite(tmp_path / "d.tif", stack, imagej=True)
+    process_flow(str(tmp_path), "d", "OneTif", 3, g["sig"], g["tsig"], g["wsig"], matlab_output=True)
+    out = tmp_path / "OpticalFlow3D" / "d"
+    c = stack.shape[0] // 2
+    rel = tf.imread_libtiff(out / f"d_rel_t{c:04d}.tiff")
+    vx = tf.imread_libtiff(out / f"d_vx_t{c:04d}.tiff")
+    assert rel.dtype == np.float64 and bits_equal(vx, g["vx"])
+    assert_rel_within(rel, g["lmin64"], g["lmax64"], 1e-10)
