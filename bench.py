@@ -9,18 +9,20 @@ five-kernel pipeline through the C-ABI (of3d_plan_execute) and leaves
 vx, vy, vz (fp64) and rel (fp32) in HBM.
 
 Default workload = BASELINE.json configs[2] (c3), the largest single-GPU
-config: 3D 512x512x128, 19 frames, xyzSig=2 tSig=3 wSig=7, fp64.  --config c2
-selects configs[1]; c4/c5 are the z-slab (strong-scaling) configs.
-N > 1 (torch.distributed.run, one rank per GPU): frame replicas — every rank
-computes its own output frame (calc_flow.py:512 marks output frames as the
-independent axis); no data-path collective; value = all ranks' voxels / max
-rank time.  Beside it, the line's "strong" object: the same frame split over
-the ranks as z-slabs (and row slabs where they carry less halo work), each
-step the newest frame's rd + rw halo exchanged over RCCL P2P beside the
-previous step's compute — per-rank compute, exchange and pipelined step times
-and the efficiency against the one-GPU frame.  Rank 0 prints ONE JSON line,
-with "parity_sample": one output crop checked against the oracle outside the
-timed region, and "build": the library's source hash (of3d_build_info).
+config: 3D 512x512x128, 19 frames, xyzSig=2 tSig=3 wSig=7, fp64, run as a time
+series (K0 batching over 5 windows; the line also carries configs[2] as stated,
+one 19-frame window with K0 every step, as single_window_ms).  --config c2
+selects configs[1]; c4/c5 are configs[3]/[4].
+N > 1 (torch.distributed.run, one rank per GPU): the north star's z-shard —
+ONE volume per output frame split over the ranks as z-slabs, the newest frame's
+rd + rw halo exchanged over RCCL P2P beside the previous step's compute — on the
+volume BASELINE names for N GPUs (c4 at N = 2 and 4, c5 at N = 8); value = the
+volume's voxels / max-over-ranks step time ("scaling": "strong").  Beside it:
+"replicas" (every rank computes the whole volume alone first: the one-GPU
+frame t1 of the split's efficiency) and "row_slabs" (the other axis).  Every
+line carries "parity_sample": one output crop checked against the oracle
+outside the timed region (on N > 1 across the cut between rank 0 and rank 1),
+and "build": the library's source hash (of3d_build_info).
 
 Roofline: the dominant kernel's average duration from HIP events recorded on
 the launch stream over the timed region (of3d_plan_set_timing ring), with its
