@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
         printf("of3d %d, %d device(s), %s\n", of3d_version(), of3d_device_count(), of3d_build_info());
         return 0;
     }
-    if (argc < 9) {
+    if (argc < 8) {
         fprintf(stderr, "usage: %s IMAGES.u16 NT NZ NY NX TAPS.f64 OUT_PREFIX [rel64]\n", argv[0]);
         return 2;
     }
