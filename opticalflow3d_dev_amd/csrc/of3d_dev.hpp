@@ -1643,11 +1643,11 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 // ---------------------------------------------------------------------------
 // K12: the gradient y, x and z passes in one kernel (calc_flow.py:279-288) — the four
 // pre-z fields never leave the CU (K1c + K2c write and re-read them through HBM).
-// Block = TY = 4 rows x TX = 128 - 2 RD output columns (128 staged columns: two waves per
-// row), marching a chunk of output planes.  Wave w: half h = w & 1 (staged column
-// c = 64 h + lane), role / row r = w >> 1.  Per input plane (one step):
+// Block = TY = 4 rows x TX = CW - 2 RD output columns (CW = 64 NWX staged columns: NWX waves
+// per row, 3 in fp64, 2 in fp32), marching a chunk of output planes.  Wave w: part h = w % NWX
+// (staged column c = 64 h + lane), role / row r = w / NWX.  Per input plane (one step):
 //   staging (LDS-DMA): the plane's TY + 2 RD rows of dt0 and of the centre frame I (the
-//     block's staged columns, 16-byte granules) go straight into LDS, a chunk of K (3, or 2
+//     block's staged columns, 16-byte granules) go straight into LDS, a chunk of K (3, 2 or 1
 //     where LDS is short) planes at a time, two chunks ahead (2 K plane slots): one chunk's loads
 //     stay in flight while the previous chunk computes; one vmcnt(0) per chunk;
 //   y passes (LDS -> registers): role 0 A1 = y(G)[dt0], role 1 A2 = y(D)[I], role 2
@@ -1668,6 +1668,21 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_byte) {
 // Needs nx * sizeof(F) and nx * sizeof(T) multiples of 16 bytes and 16-byte aligned planes.
 // ---------------------------------------------------------------------------
 constexpr int K12_TY = 4;  // rows per block
+// staged columns per block row: 64 per wave, k12_nwx waves per row.  fp64: 3 waves (192
+// staged columns, 180 outputs at rd 6): 12-wave blocks = 3 waves per SIMD instead of 2 (the
+// kernel is bound by each wave's dependent chain, so a third wave per SIMD is what pays), at
+// 168 VGPRs (one x window live at a time) and one plane per DMA chunk (LDS); and 5 % of the
+// staged columns of a 512-wide plane wasted instead of 13 %.  Same box: c3 K12 0.617 -> 0.462
+// ms, c4 4.09 -> 3.37 ms (profiles/r04/ab_k12n3/).  fp32 keeps 2 (two 8-wave blocks per CU).
+#ifndef OF3D_K12_NWX64
+#define OF3D_K12_NWX64 3
+#endif
+template <typename F>
+__host__ __device__ constexpr int k12_nwx() { return sizeof(F) == 8 ? OF3D_K12_NWX64 : 2; }
+template <typename F>
+__host__ __device__ constexpr int k12_cw() { return 64 * k12_nwx<F>(); }
+template <typename F>
+__host__ __device__ constexpr int k12_threads() { return k12_cw<F>() * K12_TY; }
 // z passes one step late (k_grad_xyz_c) in the fp32 kernels: c5 K12 18.2-18.5 -> 17.4 ms; the
 // fp64 kernel measured slower so (c3 0.602 -> 0.645 ms, same box, profiles/r03_ab/k12_defer/)
 #ifndef OF3D_K12_DEFER
@@ -1675,22 +1690,24 @@ constexpr int K12_TY = 4;  // rows per block
 #endif
 template <typename F>
 constexpr bool k12_defer() { return OF3D_K12_DEFER && sizeof(F) == 4; }
-template <int RD>
-__host__ __device__ constexpr int k12_tx() { return 128 - 2 * RD; }
-// LDS bytes of one staged plane: NRW rows of dt0 (128 + EPL columns) and of I (128 + EPL_T)
+template <typename F, int RD>
+__host__ __device__ constexpr int k12_tx() { return k12_cw<F>() - 2 * RD; }
+// LDS bytes of one staged plane: NRW rows of dt0 (CW + EPL columns) and of I (CW + EPL_T)
 template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_slot_granules() {
-    return (K12_TY + 2 * RD) * ((128 * (int)sizeof(F)) / 16 + 1 + (128 * (int)sizeof(T)) / 16 + 1);
+    return (K12_TY + 2 * RD) * ((k12_cw<F>() * (int)sizeof(F)) / 16 + 1 + (k12_cw<F>() * (int)sizeof(T)) / 16 + 1);
 }
 template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_slot_bytes() { return ((k12_slot_granules<T, F, RD>() + 63) / 64) * 1024; }
-// A tiles: [2 buffers][3 fields][even / odd copy][TY][K12_AP]; the odd copy is the row
+// A tiles: [2 buffers][3 fields][even / odd copy][TY][AP]; the odd copy is the row
 // shifted by one element, so every x-pass window starts 16-byte aligned in one of the two
 // (pairs read as ds_read_b128: 4 LDS cycles per 16 B; ds_read2_b64 costs 16).  Pitch
-// 132: the odd copy sits 128 B (mod 256) from the even one (conflict-free b128 groups).
-constexpr int K12_AP = 132;
+// CW + 4 (132 / 196): the odd copy sits 128 B (mod 256) from the even one (conflict-free
+// b128 groups).
 template <typename F>
-__host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * K12_AP * (int)sizeof(F); }
+__host__ __device__ constexpr int k12_ap() { return k12_cw<F>() + 4; }
+template <typename F>
+__host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * k12_ap<F>() * (int)sizeof(F); }
 // planes per DMA chunk: 2 where two chunks of slots + the A tiles fit 80 KiB and the
 // kernel's registers allow 4 waves per SIMD (fp32 rd 3 / 6: two 8-wave blocks per CU),
 // else 3 where they fit 160 KiB, else 2
@@ -1701,7 +1718,8 @@ template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_k() {
     if (OF3D_K12_TWO && sizeof(F) == 4 && RD <= 6 && 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 80 * 1024)
         return 2;
-    return 6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 3 : 2;
+    if (6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024) return 3;
+    return 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 2 : 1;
 }
 template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_lds_bytes() {
@@ -1709,26 +1727,27 @@ __host__ __device__ constexpr int k12_lds_bytes() {
 }
 
 template <typename T, typename F, int RD, int RS>
-__global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict__ Ic, const F* __restrict__ D0,
+__global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __restrict__ Ic, const F* __restrict__ D0,
                                                              int zin0, int nzc, int ny, int nx, DevTaps<F> tp,
                                                              F* __restrict__ G, size_t fs, int zg0, int q0, int nq,
                                                              int zc, int ntile, int nbx) {
-    constexpr int TY = K12_TY, TX = k12_tx<RD>(), NRW = TY + 2 * RD;
-    constexpr int NR = 2 * RD + 2, NRS = RD + 1, AP = K12_AP;  // ring slots; A tile pitch
+    constexpr int TY = K12_TY, TX = k12_tx<F, RD>(), NRW = TY + 2 * RD, CW = k12_cw<F>();
+    constexpr int NWX = k12_nwx<F>(), NWV = NWX * TY;  // waves per row; per block
+    constexpr int NR = 2 * RD + 2, NRS = RD + 1, AP = k12_ap<F>();  // ring slots; A tile pitch
     constexpr int AF = 2 * TY * AP, AB = 3 * AF;  // A field stride (even + odd copy), buffer stride
     static_assert(NRS >= 2 * RS + 1 && NR % NRS == 0 && NR % 2 == 0 && TX >= 8, "K12 geometry");
     constexpr int EF = 16 / (int)sizeof(F), ET = 16 / (int)sizeof(T);  // elements per granule
-    constexpr int GD = 128 / EF + 1, GI = 128 / ET + 1;                 // granules per staged row
+    constexpr int GD = CW / EF + 1, GI = CW / ET + 1;                   // granules per staged row
     constexpr int NG = NRW * (GD + GI), NJ = (NG + 63) / 64;            // granules / DMA instrs per plane
     constexpr int K = k12_k<T, F, RD>();  // planes per DMA chunk
     constexpr int SLOT = k12_slot_bytes<T, F, RD>(), NSLOT = 2 * K;
     static_assert(k12_lds_bytes<T, F, RD>() <= 160 * 1024, "K12 LDS");
-    constexpr int NJW = (NJ + 7) / 8;                                   // DMA instrs per wave per plane
+    constexpr int NJW = (NJ + NWV - 1) / NWV;                           // DMA instrs per wave per plane
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* At = reinterpret_cast<F*>(smem_raw + NSLOT * SLOT);  // [2 buffers][3 fields][even, odd][TY][AP]
     const int t = threadIdx.x, lane = t & 63;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int role = w >> 1, c = 64 * (w & 1) + lane;
+    const int role = w / NWX, c = 64 * (w % NWX) + lane;
     const int per = (ntile + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     if (tile >= ntile) return;  // block-uniform
@@ -1742,12 +1761,12 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
     const int gc = clampi(x0 - RD + c, 0, nx - 1);  // this thread's staged column (y passes)
     const int pd = gc - gd0, pi = gc - gi0;         // its LDS positions in the dt0 / I rows
     // DMA sources of this wave's instructions (plane-relative element offsets): instruction
-    // j = w + 8 i covers granules 64 j .. 64 j + 63 of the slot (dt0 rows, then I rows)
+    // j = w + NWV i covers granules 64 j .. 64 j + 63 of the slot (dt0 rows, then I rows)
     unsigned doff[NJW];
     bool isd[NJW];
 #pragma unroll
     for (int i = 0; i < NJW; ++i) {
-        const int g = min(64 * (w + 8 * i) + lane, NG - 1);
+        const int g = min(64 * (w + NWV * i) + lane, NG - 1);
         if (g < NRW * GD) {
             const int r = g / GD, q = g - r * GD;
             isd[i] = true;
@@ -1765,9 +1784,9 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
         const unsigned sb = lds0 + (unsigned)((s % NSLOT) * SLOT);
 #pragma unroll
         for (int i = 0; i < NJW; ++i) {
-            if (w + 8 * i < NJ) {
+            if (w + NWV * i < NJ) {
                 const void* src = isd[i] ? (const void*)(D0 + pz + doff[i]) : (const void*)(Ic + pz + doff[i]);
-                glds16(src, __builtin_amdgcn_readfirstlane(sb + (unsigned)((w + 8 * i) * 1024)));
+                glds16(src, __builtin_amdgcn_readfirstlane(sb + (unsigned)((w + NWV * i) * 1024)));
             }
         }
     };
@@ -1901,20 +1920,52 @@ __global__ __launch_bounds__(128 * K12_TY) void k_grad_xyz_c(const T* __restrict
                             x[2 * i + 1] = v2.y;
                         }
                     };
-                    F x1[2 * RD + 2], x2[2 * RS + 2], x3[2 * RD + 2];
-                    window.template operator()<RD>(0, x1);
-                    window.template operator()<RS>(1, x2);
-                    window.template operator()<RD>(2, x3);
-                    F b1 = x1[RD] * hg[0], b2 = x2[RS] * hs[0], b3 = x3[RD] * hd[0], b4 = x3[RD] * hs[0];
+                    F b1, b2, b3, b4;
+                    if constexpr (NWX == 3) {
+                        // 12-wave blocks (168 VGPRs): one x window live at a time, each window's
+                        // reads pinned behind the previous field's pass (3 waves per SIMD hide
+                        // the three LDS round trips)
+                        {
+                            F x1[2 * RD + 2];
+                            window.template operator()<RD>(0, x1);
+                            b1 = x1[RD] * hg[0];
 #pragma unroll
-                    for (int k = RD; k >= 1; --k) {
-                        b1 = b1 + (x1[RD - k] + x1[RD + k]) * hg[k];
-                        b3 = b3 + (x3[RD - k] - x3[RD + k]) * hd[k];
-                    }
+                            for (int k = RD; k >= 1; --k) b1 = b1 + (x1[RD - k] + x1[RD + k]) * hg[k];
+                        }
+                        asm volatile("" : "+v"(b1)::"memory");
+                        {
+                            F x3[2 * RD + 2];
+                            window.template operator()<RD>(2, x3);
+                            b3 = x3[RD] * hd[0], b4 = x3[RD] * hs[0];
 #pragma unroll
-                    for (int k = RS; k >= 1; --k) {
-                        b2 = b2 + (x2[RS - k] + x2[RS + k]) * hs[k];
-                        b4 = b4 + (x3[RD - k] + x3[RD + k]) * hs[k];
+                            for (int k = RD; k >= 1; --k) b3 = b3 + (x3[RD - k] - x3[RD + k]) * hd[k];
+#pragma unroll
+                            for (int k = RS; k >= 1; --k) b4 = b4 + (x3[RD - k] + x3[RD + k]) * hs[k];
+                        }
+                        asm volatile("" : "+v"(b3), "+v"(b4)::"memory");
+                        {
+                            F x2[2 * RS + 2];
+                            window.template operator()<RS>(1, x2);
+                            b2 = x2[RS] * hs[0];
+#pragma unroll
+                            for (int k = RS; k >= 1; --k) b2 = b2 + (x2[RS - k] + x2[RS + k]) * hs[k];
+                        }
+                    } else {
+                        F x1[2 * RD + 2], x2[2 * RS + 2], x3[2 * RD + 2];
+                        window.template operator()<RD>(0, x1);
+                        window.template operator()<RS>(1, x2);
+                        window.template operator()<RD>(2, x3);
+                        b1 = x1[RD] * hg[0], b2 = x2[RS] * hs[0], b3 = x3[RD] * hd[0], b4 = x3[RD] * hs[0];
+#pragma unroll
+                        for (int k = RD; k >= 1; --k) {
+                            b1 = b1 + (x1[RD - k] + x1[RD + k]) * hg[k];
+                            b3 = b3 + (x3[RD - k] - x3[RD + k]) * hd[k];
+                        }
+#pragma unroll
+                        for (int k = RS; k >= 1; --k) {
+                            b2 = b2 + (x2[RS - k] + x2[RS + k]) * hs[k];
+                            b4 = b4 + (x3[RD - k] + x3[RD + k]) * hs[k];
+                        }
                     }
                     r1[j % NR] = b1;
                     r4[j % NR] = b4;

@@ -789,7 +789,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     // 16-plane marches re-form 12 halo planes each, K1c + K2c measured faster; c3: K12 0.62 vs
     // 0.83 ms); OF3D_K12=1 forces it, OF3D_K12=0 disables it
     const char* k12_env = getenv("OF3D_K12");
-    const int k12_tiles = (int)cdiv(nx, 128 - 2 * p->rd) * (int)cdiv(ny, K12_TY);
+    const int k12_tiles = (int)cdiv(nx, k12_cw<F>() - 2 * p->rd) * (int)cdiv(ny, K12_TY);
     const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
     // (fp32 plans, rd <= 6: two blocks per CU — c3 0.27 + 0.36 ms vs K1c + K2c 0.43 + 0.25, c5
     // 12.7 + 21.3 vs 23.5 + 13.2; rd 9 in fp32 runs one block per CU: K1c + K2c)
@@ -932,7 +932,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             const void* Ic = (const char*)d_frames[p->rt] + (size_t)(R.zb0 - frame_z0) * plane * es;
             const F* D0c = D0b;
             F* Go = Y;
-            const int tx = p->rd == 3 ? k12_tx<3>() : (p->rd == 6 ? k12_tx<6>() : k12_tx<9>());
+            const int tx = k12_cw<F>() - 2 * p->rd;
             int nbx = (int)cdiv(nx, tx), ntile = nbx * (int)cdiv(ny, K12_TY);
             int zin0 = (int)R.zb0, nzc = (int)R.zb1, zg0 = (int)R.zg0, qa = (int)q0, nq = ng;
             // planes per block: the longest march (up to 256) that still gives >= 1024 blocks
@@ -942,14 +942,16 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             int zc = zc_env ? atoi(zc_env) : 0;
             if (zc <= 0) {
                 zc = 256;
-                while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;
+                // (three full rounds of one block per CU for the 12-wave fp64 blocks)
+                const long kmin = k12_nwx<F>() == 3 ? 768 : 1024;
+                while (zc > 16 && (long)ntile * cdiv(nq, zc) < kmin) zc /= 2;
             }
             const unsigned gx = 8 * cdiv(ntile, 8);
             const size_t lds = k12_lds<F>(dtype, p->rd);
             void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&zin0, (void*)&nzc, (void*)&ny, (void*)&nx, (void*)&tp,
                             (void*)&Go, (void*)&fs, (void*)&zg0, (void*)&qa, (void*)&nq, (void*)&zc, (void*)&ntile,
                             (void*)&nbx};
-            OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(128 * K12_TY), args, lds, st));
+            OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(k12_threads<F>()), args, lds, st));
             p->used |= KU_K12;
             return 0;
         }
