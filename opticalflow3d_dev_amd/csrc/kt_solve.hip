@@ -40,6 +40,7 @@ const void* k5c_fn(int rw, int nb, int r, int nw, int rt0) {
 template <typename RelT>
 const void* k5c2_fn(int rw, int nb, int r) {
     if (const char* e = getenv("OF3D_K5C_PK"); !(e && e[0] == '1')) return nullptr;
+    if (r != 4 && r != 8) return nullptr;  // instances at R 4 / 8 only (the caller's grid follows r)
 #define OF3D_K5C2(RW) \
     case RW:                                                                                            \
         if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c2<RelT, RW, 3, 4> : nullptr;              \

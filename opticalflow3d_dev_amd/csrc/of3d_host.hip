@@ -346,6 +346,8 @@ int k5c_setup(of3d_plan* p) {
     // planes per z-group: 8 (64-plane blocks) or 4 (32).  A 128-plane fp32 instance (R 16, 4 waves,
     // 191 VGPRs, two blocks per CU) measured slower: c5 fp32 41.8 vs 39.7 ms, c3 fp32 0.74 vs 0.68
     int r = er ? atoi(er) : 8;
+    // 6 planes (48-plane blocks, 160 VGPRs: three blocks per CU) measured slower: c3 K5c 1.00 ->
+    // 1.05 ms, c4 7.17 -> 7.30, c5 fp32 34.7 -> 35.8 (profiles/r04/ab_k5r6/)
     if (r != 4) r = 8;  // the instances compiled (k5c_fn): the launch grid must match them
     // fp32: the packed kernel (two columns per lane as float2; window bytes as the fp64 kernel's)
     const void* pk = nullptr;
@@ -368,6 +370,7 @@ int k5c_setup(of3d_plan* p) {
     const char* enw = getenv("OF3D_K5C_NW");
     int nw = enw ? atoi(enw) : 4;
     if (nw != 8) nw = 4;
+    if (nw == 8) r = 8;  // the 8-wave instances are R 8 only (k5c_fn): grid and LDS follow r
     size_t buf = (size_t)k5c_groups<F>(p->rw, r, nw) * 1024;
     int nb = nw == 8 ? (3 * buf <= 160 * 1024 ? 3 : 0) : (2 * 3 * buf <= 160 * 1024 ? 3 : 2);  // 4 waves: two blocks per CU
     const void* fn = nb ? (p->rel64 ? k5c_fn<F, double>(p->rw, nb, r, nw) : k5c_fn<F, float>(p->rw, nb, r, nw)) : nullptr;

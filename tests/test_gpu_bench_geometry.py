@@ -157,7 +157,10 @@ def k34_candidates(d_in, p, mode=0):
 
 
 FAMILIES = [dict(OF3D_K34_UQ=0), dict(OF3D_K34_UQ=1), dict(OF3D_K34_UQ=2), dict(OF3D_K5C_NW=8),
-            dict(OF3D_K5C_R=4), dict(OF3D_K12=0), dict(OF3D_K34_TUNE=0)]
+            dict(OF3D_K5C_R=4), dict(OF3D_K12=0), dict(OF3D_K34_TUNE=0),
+            # both K5c knobs at once: the 8-wave instances are R 8 only, so the host's grid and
+            # LDS must follow R 8 too (a 4-plane grid over the 8-plane kernel once gave garbage)
+            dict(OF3D_K5C_R=4, OF3D_K5C_NW=8)]
 
 
 def test_c3_every_kernel_family_bit_identical(c3):
