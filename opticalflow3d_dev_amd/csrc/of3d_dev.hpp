@@ -1829,7 +1829,9 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                 for (int k = R; k >= 1; --k)
                     o = o + (ANTI ? (v[r + RD - k] - v[r + RD + k]) : (v[r + RD - k] + v[r + RD + k])) * h[k];
                 a[r * AP] = o;
-                if (c > 0) a[TY * AP + r * AP - 1] = o;
+                // odd copy at c - 1; lane c = 0 writes the pad column AP - 1 of the row before
+                // (even copy's last row for r = 0), which no window reads: no exec mask
+                a[TY * AP + r * AP - 1] = o;
             }
         };
         if (role == 0)
