@@ -1038,6 +1038,13 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 #ifndef OF3D_K34WS_PD
 #define OF3D_K34WS_PD 2
 #endif
+// the producers' two row chains side by side (fp64 k_prod_wyx_ws): without the two empty asm
+// fences the scheduler issued half of phase A's ops right behind the op they depend on; with
+// them 2 %.  Same ops, same order per chain (bit-identical).  c3 K34 1.665 -> 1.631 ms, c4
+// equal (profiles/r04/ab_k34ilp/).  The packed fp32 kernel spills with it and keeps its form.
+#ifndef OF3D_K34_ILP
+#define OF3D_K34_ILP 1
+#endif
 #ifndef OF3D_K34WS_DB
 #define OF3D_K34WS_DB 2
 #endif
@@ -1146,8 +1153,21 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                                     ring[ic1 % NR] = p1;
 #pragma unroll
                                     for (int k = RW - 1; k >= 1; --k) {
+#if OF3D_K34_ILP
+                                        // the two rows' chains side by side (the scheduler otherwise
+                                        // runs half the ops back to back on their predecessor)
+                                        F s0 = ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR];
+                                        F s1 = ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR];
+                                        asm volatile("" : "+v"(s0), "+v"(s1));
+                                        s0 = s0 * h[k];
+                                        s1 = s1 * h[k];
+                                        asm volatile("" : "+v"(s0), "+v"(s1));
+                                        a0 = a0 + s0;
+                                        a1 = a1 + s1;
+#else
                                         a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
                                         a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
+#endif
                                     }
                                     tile[k34_row(j % S, cwp) + wpos] = a0;
                                     tile[k34_row((j + 1) % S, cwp) + wpos] = a1;
