@@ -675,6 +675,15 @@ def parity_box(dims, axis, cut, size=16, dx=44):
     return tuple(box)
 
 
+def device_used_gb(dev):
+    """Device memory in use on `dev` right now (every allocator: torch's and the plans'
+    hipMalloc), from hipMemGetInfo, GB."""
+    import torch
+
+    free, total = torch.cuda.mem_get_info(dev)
+    return round((total - free) / 1e9, 2), round(total / 1e9, 2)
+
+
 def slab_on_every_rank(world, dev, *a, **kw):
     """SlabBench(*a, **kw) on every rank, or on none: the ranks agree (a MAX over ranks) before
     any of them starts timed steps, so a rank that cannot allocate its part (device memory)
@@ -706,6 +715,9 @@ def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=Tru
     nt, nz, ny, nx, s, t, w, _ = CONFIGS[cfg]
     sb = slab_on_every_rank(world, dev, (nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32,
                             seed=20260206 + 50, pipeline=pipeline, k0_batch=k0_batch)
+    used = device_used_gb(dev)[0]
+    if world > 1:
+        used = max_over_ranks([used], dev)[0]
     try:
         comp = timed_steps(lambda: sb.step(exchange=False), steps, warmup, world, dev)
         xchg = timed_steps(lambda: sb.step(compute=False), steps, warmup, world, dev)
@@ -720,7 +732,7 @@ def strong_split(cfg, axis, world, rank, dev, steps, warmup, t1_ms, pipeline=Tru
             "ms_per_step": round(ms, 5), "value": round(nz * ny * nx / (ms * 1e-3) / 1e6, 3), "unit": "Mvoxels/s",
             "compute_ms_max_rank": round(comp / steps * 1e3, 5), "exchange_ms": round(xchg / steps * 1e3, 5),
             "efficiency_vs_one_gpu_frame": round(t1_ms / (world * ms), 4) if t1_ms else None,
-            "outputs_finite_rank0": finite, "parity_sample": par}
+            "device_used_GB_max_rank": used, "outputs_finite_rank0": finite, "parity_sample": par}
 
 
 def replica_frame(cfg, world, rank, dev, steps, warmup, fp32, pipeline, k0_batch):
@@ -733,14 +745,17 @@ def replica_frame(cfg, world, rank, dev, steps, warmup, fp32, pipeline, k0_batch
     sb = slab_on_every_rank(world, dev, (nz, ny, nx), (s, t, w), 0, rank, world, dev, fp32=fp32, vrank=(0, 1),
                             seed=20260206 + 60 + rank, pipeline=pipeline, k0_batch=k0_batch)
     try:
+        used, total = device_used_gb(dev)
         el = timed_steps(sb.step, steps, warmup, world, dev)
     finally:
         sb.close()
         del sb
         torch.cuda.empty_cache()
     ms = el / steps * 1e3
+    if world > 1:
+        used = max_over_ranks([used], dev)[0]
     return {"ms_per_step": round(ms, 5), "value": round(world * nz * ny * nx / (ms * 1e-3) / 1e6, 3),
-            "unit": "Mvoxels/s", "scaling": "weak",
+            "unit": "Mvoxels/s", "scaling": "weak", "device_used_GB": used, "device_total_GB": total,
             "what": f"{world} one-GPU frames at once (every rank its own whole volume), max over ranks"}
 
 
@@ -777,8 +792,15 @@ def run_slab(args, world, rank, local_rank, dev):
             replicas = {"error": f"{type(e).__name__}: {e}"[:300]}
             torch.cuda.empty_cache()
     seed = 20260206 + (5 if fp32 else 4)
+    # the replicas' whole-volume plan, ring and outputs must be gone before the split allocates
+    # (c5 at N = 8: ~266 GB of 288 per GPU for the replica, then the slab plans)
+    base_used, total_gb = device_used_gb(dev)
+    # (one GPU per rank under RCCL; gloo rehearsals share a device between ranks)
+    if replicas is not None and os.environ.get("OF3D_BENCH_BACKEND", "nccl") == "nccl" and base_used > 8.0:
+        raise RuntimeError(f"replica buffers not freed before the split: {base_used} GB still in use")
     sb = SlabBench((nz, ny, nx), (s, t, w), axis, rank, world, dev, fp32=fp32, timing=max(args.steps, 1),
                    vrank=(prank, pworld) if vr else None, seed=seed, pipeline=not args.no_pipeline, k0_batch=kb)
+    split_used = device_used_gb(dev)[0]
     plan = sb.plan
 
     def align():
@@ -788,7 +810,7 @@ def run_slab(args, world, rank, local_rank, dev):
     elapsed, profile, dom, dom_ms = timed_region(sb.step, plan, args, world, dev, align=align if sb.batch else None)
     finite = sb.finite()
     if world > 1:
-        elapsed, bad = max_over_ranks([elapsed, 0.0 if finite else 1.0], dev)
+        elapsed, bad, split_used = max_over_ranks([elapsed, 0.0 if finite else 1.0, split_used], dev)
         finite = bad == 0.0
     parity = None if args.no_parity_sample or vr else slab_parity(sb, fp32)
     split_detail = None
@@ -828,6 +850,13 @@ def run_slab(args, world, rank, local_rank, dev):
                         (nwin * 2 + 3 * sv + 4) * own, frame_ops_per_voxel(rd, rs, rt, rw) * own, nwin, sv,
                         used=kernels)
         roof["frame"]["note"] = "this rank's share: " + describe
+        if world > 1 or vr:
+            # the committed PMC profile measured a whole-volume launch: its bytes do not describe
+            # this rank's slab launch (fewer planes + the halo), and no slab PMC pass exists
+            whole = roof["traffic"]
+            roof["traffic"] = None
+            roof["traffic_note"] = (f"not measured for slab launches (profiles/pmc_{cfg}.json is the whole-volume "
+                                    f"launch: {whole} B); kernel_hbm.workspace_bytes_per_launch is this slab's")
         cpu = None
         if world == 1 and not vr and not args.no_cpu_baseline:
             sub = cpu_sample_planes(nz, ny, nx, args.cpu_budget)
@@ -855,6 +884,9 @@ def run_slab(args, world, rank, local_rank, dev):
                        "series": (f"K0 batching: {kb} windows per K0 pass (of3d_plan_execute_ahead)") if kb >= 2 else
                                  ("frame pipelining (of3d_plan_execute_next)" if not args.no_pipeline else "plain")},
             "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "build": build_stamp(),
+            "memory": {"device_total_GB": total_gb, "before_split_GB": base_used,
+                       "split_GB_max_rank": split_used,
+                       "replicas_GB_max_rank": (replicas or {}).get("device_used_GB")},
         }
         if split_detail is not None:
             line["split"] = split_detail

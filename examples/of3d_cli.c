@@ -16,12 +16,16 @@
 
 #include "of3d.h"
 
+/* a regular file whole (NULL for anything ftell cannot size: pipes, FIFOs, errors) */
 static void* read_file(const char* path, size_t* n) {
     FILE* f = fopen(path, "rb");
     if (!f) return NULL;
-    fseek(f, 0, SEEK_END);
-    long len = ftell(f);
-    fseek(f, 0, SEEK_SET);
+    long len = -1;
+    if (fseek(f, 0, SEEK_END) == 0) len = ftell(f);
+    if (len < 0 || fseek(f, 0, SEEK_SET) != 0) {
+        fclose(f);
+        return NULL;
+    }
     void* buf = malloc(len > 0 ? (size_t)len : 1);
     if (buf && fread(buf, 1, (size_t)len, f) != (size_t)len) {
         free(buf);
@@ -52,6 +56,10 @@ int main(int argc, char** argv) {
         return 2;
     }
     const int64_t nt = atoll(argv[2]), nz = atoll(argv[3]), ny = atoll(argv[4]), nx = atoll(argv[5]);
+    if (nt < 1 || nz < 1 || ny < 1 || nx < 1 || nz > 65535 || ny * nx > INT32_MAX) {
+        fprintf(stderr, "of3d_cli: bad dimensions\n");
+        return 2;
+    }
     const int rel64 = argc > 8 && strcmp(argv[8], "rel64") == 0;
     size_t ni = 0, nt_ = 0;
     uint16_t* img = (uint16_t*)read_file(argv[1], &ni);
@@ -60,26 +68,38 @@ int main(int argc, char** argv) {
         fprintf(stderr, "of3d_cli: bad input files\n");
         return 2;
     }
+    /* radii: whole numbers in [0, 4096] (rt <= 32, the library's limits) before any pointer
+       arithmetic on them, and the file must hold exactly the taps they announce */
+    for (int i = 0; i < 4; ++i)
+        if (!(tp[i] >= 0.0 && tp[i] <= (i == 2 ? 32.0 : 4096.0)) || tp[i] != (double)(int)tp[i]) {
+            fprintf(stderr, "of3d_cli: bad tap radius in the taps header\n");
+            return 2;
+        }
     of3d_taps taps;
     taps.rd = (int)tp[0];
     taps.rs = (int)tp[1];
     taps.rt = (int)tp[2];
     taps.rw = (int)tp[3];
+    const size_t ntaps = 4 + (size_t)(2 * taps.rd + 1) * 2 + (2 * taps.rs + 1) + (2 * taps.rt + 1) + (2 * taps.rw + 1);
+    if (ntaps * sizeof(double) != nt_) {
+        fprintf(stderr, "of3d_cli: taps file size does not match its radii\n");
+        return 2;
+    }
     const double* q = tp + 4;
     taps.gauss = q, q += 2 * taps.rd + 1;
     taps.deriv = q, q += 2 * taps.rd + 1;
     taps.smooth = q, q += 2 * taps.rs + 1;
     taps.tderiv = q, q += 2 * taps.rt + 1;
-    taps.window = q, q += 2 * taps.rw + 1;
-    if ((size_t)(q - tp) * sizeof(double) != nt_) {
-        fprintf(stderr, "of3d_cli: taps file size does not match its radii\n");
-        return 2;
-    }
+    taps.window = q;
     const size_t nv = (size_t)(nz * ny * nx);
     double* vx = (double*)malloc(nv * sizeof(double));
     double* vy = (double*)malloc(nv * sizeof(double));
     double* vz = (double*)malloc(nv * sizeof(double));
     void* rel = malloc(nv * (rel64 ? sizeof(double) : sizeof(float)));
+    if (!vx || !vy || !vz || !rel) {
+        fprintf(stderr, "of3d_cli: out of host memory\n");
+        return 1;
+    }
     of3d_perf perf;
     if (of3d_flow3d(img, OF3D_U16, nt, nz, ny, nx, &taps, rel64 ? OF3D_REL_F64 : OF3D_FP64_EXACT, 0, vx, vy, vz, rel,
                     &perf) != 0) {

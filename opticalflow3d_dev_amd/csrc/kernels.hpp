@@ -21,5 +21,4 @@ template <int NP> const void* k34_fn_pk(int rw, int s);                        /
 template <typename F, typename RelT> const void* k5_kernel(int rw);          // kt_solve_legacy.hip
 template <typename F, typename RelT> const void* k5_dma_kernel(int rw, int nb);  // kt_solve_legacy.hip
 template <typename F, typename RelT> const void* k5c_fn(int rw, int nb, int r, int nw, int rt0 = 0);  // kt_solve.hip
-template <typename RelT> const void* k5c2_fn(int rw, int nb, int r);            // kt_solve.hip (packed fp32)
 }  // namespace of3dk

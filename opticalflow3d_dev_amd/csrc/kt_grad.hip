@@ -7,7 +7,6 @@ namespace of3dk {
 // compile-time-rt K0 instances: u8 / u16 / f32 input, rt 3, 6, 9 (tSig 1, 2, 3)
 template <typename F>
 const void* k0c_fn(int dtype, int rt) {
-    if (const char* e = getenv("OF3D_K0C"); e && e[0] == '0') return nullptr;
 #define OF3D_K0C(T)                                                   \
     if (rt == 3) return (const void*)k_tderiv_vec_c<T, F, 3>;        \
     if (rt == 6) return (const void*)k_tderiv_vec_c<T, F, 6>;        \

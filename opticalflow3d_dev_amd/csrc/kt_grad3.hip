@@ -8,7 +8,6 @@ namespace of3dk {
 // fp32 only at rd 9; other radii / dtypes run K1c + K2c (or the older kernels).
 template <typename F>
 const void* k12_fn(int dtype, int rd, int rs) {
-    if (const char* e = getenv("OF3D_K12"); e && e[0] == '0') return nullptr;
 #define OF3D_K12(T)                                                                \
     if (rd == 3 && rs == 1) return (const void*)k_grad_xyz_c<T, F, 3, 1>;          \
     if (rd == 6 && rs == 2) return (const void*)k_grad_xyz_c<T, F, 6, 2>;          \

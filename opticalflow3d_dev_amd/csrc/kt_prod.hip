@@ -48,7 +48,6 @@ const void* k34_fn_uq(int rw, int s) {
 // columns, 128 VGPRs)
 template <typename F, int NP>
 const void* k34_fn_ws(int rw, int s) {
-    if (const char* e = getenv("OF3D_K34_WS"); e && e[0] == '0') return nullptr;
 #define OF3D_K34W(RW)                                                              \
     if (rw == RW) {                                                                \
         if (s == 8) return (const void*)k_prod_wyx_ws<F, NP, RW, 8>;               \
@@ -66,7 +65,6 @@ const void* k34_fn_ws(int rw, int s) {
 // Packed-fp32 instances (k_prod_wyx_pk: 4 producer + 4 consumer waves on float2 lanes)
 template <int NP>
 const void* k34_fn_pk(int rw, int s) {
-    if (const char* e = getenv("OF3D_K34_PK"); e && e[0] == '0') return nullptr;
 #define OF3D_K34P(RW)                                                      \
     if (rw == RW) {                                                        \
         if (s == 8) return (const void*)k_prod_wyx_pk<NP, RW, 8>;          \

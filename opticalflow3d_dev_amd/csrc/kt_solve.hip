@@ -33,31 +33,6 @@ const void* k5c_fn(int rw, int nb, int r, int nw, int rt0) {
 #undef OF3D_K5C
 }
 
-// packed-fp32 K5c (OF3D_FP32 plans): same radii and geometry choices.  Opt-in
-// (OF3D_K5C_PK=1): bit-identical, half the pass instructions, but measured no faster
-// (c3 fp32 0.66 vs 0.63 ms, c5 41.6 vs 40.4 ms) — the fp32 K5c is bound by its window
-// traffic and the fp64 solve, not by fp32 issue.
-template <typename RelT>
-const void* k5c2_fn(int rw, int nb, int r) {
-    if (const char* e = getenv("OF3D_K5C_PK"); !(e && e[0] == '1')) return nullptr;
-    if (r != 4 && r != 8) return nullptr;  // instances at R 4 / 8 only (the caller's grid follows r)
-#define OF3D_K5C2(RW) \
-    case RW:                                                                                            \
-        if (r == 4) return nb == 3 ? (const void*)k_wz_solve_c2<RelT, RW, 3, 4> : nullptr;              \
-        return nb == 3 ? (const void*)k_wz_solve_c2<RelT, RW, 3, 8> : (const void*)k_wz_solve_c2<RelT, RW, 2, 8>;
-    switch (rw) {
-        OF3D_K5C2(9)
-        OF3D_K5C2(12)
-        OF3D_K5C2(15)
-        OF3D_K5C2(18)
-        OF3D_K5C2(21)
-        default: return nullptr;
-    }
-#undef OF3D_K5C2
-}
-
-template const void* k5c2_fn<float>(int, int, int);
-template const void* k5c2_fn<double>(int, int, int);
 template const void* k5c_fn<double, float>(int, int, int, int, int);
 template const void* k5c_fn<double, double>(int, int, int, int, int);
 template const void* k5c_fn<float, float>(int, int, int, int, int);

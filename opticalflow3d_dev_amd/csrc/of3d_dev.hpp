@@ -42,6 +42,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -399,11 +400,8 @@ struct K0Next {
 // ---------------------------------------------------------------------------
 constexpr int K1_R = 4, K1_TY = 4 * K1_R, K1_NZB = 4;
 
-#ifndef OF3D_K1_OCC
-#define OF3D_K1_OCC 3
-#endif
 template <typename T, typename F, int NJ>
-__global__ __launch_bounds__(256, OF3D_K1_OCC) void k_grad_xy(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
+__global__ __launch_bounds__(256, 3) void k_grad_xy(const T* __restrict__ Ic, const F* __restrict__ D0, int ny,
                                                  int nx, int nzp, DevTaps<F> tp, F* __restrict__ B, size_t fs,
                                                  int need_b4) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -722,13 +720,10 @@ __global__ __launch_bounds__(256, TJ == 1 ? 3 : 2) void k_wx(const F* __restrict
 // ---------------------------------------------------------------------------
 constexpr int k34_nr(int rw, int s) { return ((2 * rw + 2 + s - 1) / s) * s; }
 // K34 block -> (plane zl, row chunk yc, column block bx, product p).  The linear workgroup id
-// b runs on XCD b % 8 (round-robin dispatch), so blocks that should share an L2 share b % 8.
-//   cpg > 0 (plane-major, the default): group g = (plane, run of cpg row chunks) =
-//     (b / 8 / mb) * 8 + b % 8, members (chunk in the run, product, column block); ngroups = groups.
-//   cpg < 0 (chunk-major, OF3D_K34_CM): XCD x runs planes x, x + 8, ..., each plane's row
-//     chunks one after another, every chunk's NP x nbx blocks dispatched together — the rows in
-//     flight on an XCD are one chunk's (and its 2 RW halo rows, the previous chunk's last rows);
-//     ngroups = planes.
+// b runs on XCD b % 8 (round-robin dispatch), so blocks that should share an L2 share b % 8:
+// group g = (plane, run of cpg row chunks) = (b / 8 / mb) * 8 + b % 8, members (chunk in the
+// run, product, column block).  (A chunk-major order — each XCD running its planes' row chunks
+// one after another — measured slower everywhere, round 4: profiles/r04/ab_k34_cm.txt.)
 struct K34Blk {
     int zl, yc, bx, p;
     bool ok;
@@ -737,15 +732,6 @@ template <int NP>
 __device__ __forceinline__ K34Blk k34_block(int nbx, int nyb, int cpg, int ngroups) {
     const int kb = blockIdx.x >> 3, xcd = blockIdx.x & 7;
     K34Blk r;
-    if (cpg < 0) {
-        const int mb = NP * nbx, k = kb / mb, m = kb % mb;
-        r.bx = m % nbx;
-        r.p = m / nbx;
-        r.zl = xcd + 8 * (k / nyb);
-        r.yc = k % nyb;
-        r.ok = r.zl < ngroups;
-        return r;
-    }
     const int mb = cpg * NP * nbx;
     const int g = (kb / mb) * 8 + xcd;
     int m = kb % mb;
@@ -785,9 +771,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-#ifndef OF3D_K34_OCC
-#define OF3D_K34_OCC 3
-#endif
 
 // Raw buffer access (one SGPR descriptor per plane-field, 32-bit SGPR row offset +
 // one VGPR lane offset): no per-load 64-bit address VALU, no address VGPRs.
@@ -801,13 +784,9 @@ __device__ __forceinline__ F buf_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, uns
     else
         return __builtin_bit_cast(F, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
-// Cache policy of the buffer stores: OF3D_ST_NT=1 marks them non-temporal (gfx950 "nt":
-// streamed past L2 residency; every stored field is re-read only by a later kernel).  Measured
-// neutral (c3 fp64 3.707 vs 3.718 ms, c3 fp32 2.071 vs 2.110, c5 fp32 120.65 vs 120.76): off.
-#ifndef OF3D_ST_NT
-#define OF3D_ST_NT 0
-#endif
-constexpr int kStAux = OF3D_ST_NT ? 2 : 0;
+// Buffer stores with the default cache policy (non-temporal stores measured neutral: c3 fp64
+// 3.707 vs 3.718 ms, c5 fp32 120.65 vs 120.76; every stored field is re-read by a later kernel).
+constexpr int kStAux = 0;
 template <typename F>
 __device__ __forceinline__ void buf_st(F v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
     if constexpr (sizeof(F) == 8)
@@ -839,7 +818,7 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
 // OCC: waves per SIMD the register budget is cut for (3: 168 VGPRs; 2: 256, for 8-wave blocks,
 // which run one per CU anyway); PDX: gradient prefetch rows (0: as far as OCC 3 allows);
 // DB: LDS prefetch distance of the phase-B pass; UQ: staging (below).
-template <typename F, int NP, int RW, int S, int RB = 4, int OCC = OF3D_K34_OCC, int PDX = 0, int DB = 2,
+template <typename F, int NP, int RW, int S, int RB = 4, int OCC = 3, int PDX = 0, int DB = 2,
           bool UQ = false>
 __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
                                                        int nx, size_t fs, const F* __restrict__ hw, int tx,
@@ -848,11 +827,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
     constexpr int PD0 = PDX ? PDX : (sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8));
-#ifdef OF3D_K34_PD
-    constexpr int PD = NR % OF3D_K34_PD == 0 ? OF3D_K34_PD : PD0;  // experiments
-#else
     constexpr int PD = PD0;
-#endif
     // RB: W-x outputs per phase-B item (RB 2 measured slower: c2 +16 %, c3 +15 %; not instantiated)
     constexpr unsigned ES = sizeof(F);
     static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
@@ -1035,20 +1010,11 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // K5c itself, not its access pattern, is the cost.
 // (12-wave blocks — 4 consumer waves, 168 VGPRs, deeper prefetch, 8-row tiles — measured
 // slower: c3 1.95 vs 1.72 ms, c2 0.27 vs 0.19: the 16-wave occupancy hides more.)
-#ifndef OF3D_K34WS_PD
-#define OF3D_K34WS_PD 2
-#endif
-// the producers' two row chains side by side (fp64 k_prod_wyx_ws): without the two empty asm
-// fences the scheduler issued half of phase A's ops right behind the op they depend on; with
-// them 2 %.  Same ops, same order per chain (bit-identical).  c3 K34 1.665 -> 1.631 ms, c4
-// equal (profiles/r04/ab_k34ilp/).  The packed fp32 kernel spills with it and keeps its form.
-#ifndef OF3D_K34_ILP
-#define OF3D_K34_ILP 1
-#endif
-#ifndef OF3D_K34WS_DB
-#define OF3D_K34WS_DB 2
-#endif
-template <typename F, int NP, int RW, int S, int PD = OF3D_K34WS_PD, int DB = OF3D_K34WS_DB>
+// The producers' two row chains side by side: without the two empty asm fences in phase A the
+// scheduler issued half of its ops right behind the op they depend on; with them 2 %.  Same ops,
+// same order per chain (bit-identical).  c3 K34 1.665 -> 1.631 ms, c4 equal
+// (profiles/r04/ab_k34ilp/).  The packed fp32 kernel spills with it and keeps its form.
+template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2>
 __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
                                                       size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
                                                       int nyb, int cpg, int ngroups, int yb0, int yb1) {
@@ -1153,7 +1119,6 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                                     ring[ic1 % NR] = p1;
 #pragma unroll
                                     for (int k = RW - 1; k >= 1; --k) {
-#if OF3D_K34_ILP
                                         // the two rows' chains side by side (the scheduler otherwise
                                         // runs half the ops back to back on their predecessor)
                                         F s0 = ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR];
@@ -1164,10 +1129,6 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                                         asm volatile("" : "+v"(s0), "+v"(s1));
                                         a0 = a0 + s0;
                                         a1 = a1 + s1;
-#else
-                                        a0 = a0 + (ring[(j + RW - k) % NR] + ring[(j + RW + k) % NR]) * h[k];
-                                        a1 = a1 + (ring[(j + 1 + RW - k) % NR] + ring[(j + 1 + RW + k) % NR]) * h[k];
-#endif
                                     }
                                     tile[k34_row(j % S, cwp) + wpos] = a0;
                                     tile[k34_row((j + 1) % S, cwp) + wpos] = a1;
@@ -1225,9 +1186,6 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
 // producer's two rows j, j + 1 of columns c, c + 1 are the pair row j / 2 at x = c, c + 1.
 // Pair pitch P2 = 1 (mod 32) float2: the consumers' 4 pairs x 4 segments of a 16-lane
 // group hit 32 distinct banks.  Ring, prefetch and tile double-buffering as k_prod_wyx_ws.
-#ifndef OF3D_K34PK_LD64
-#define OF3D_K34PK_LD64 1
-#endif
 template <int NP, int RW, int S, int PD = 2, int DB = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_prod_wyx_pk(const float* __restrict__ G, float* __restrict__ Q, int ny,
                                                      int nx, size_t fs, const float* __restrict__ hw, int tx,
@@ -1257,12 +1215,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // producer waves with no staged column pair: every wave still takes one barrier per tile
     // (a wave-uniform test, so the whole wave takes this branch)
     if (prod && __builtin_amdgcn_readfirstlane(t >> 6) >= wa) {
-        for (int tt = 0; tt < (nrows + S - 1) / S; ++tt) {
-            lds_barrier();
-#ifdef OF3D_K34PK_SYNC2
-            lds_barrier();
-#endif
-        }
+        for (int tt = 0; tt < (nrows + S - 1) / S; ++tt) lds_barrier();
         return;
     }
     f2 h[RW + 1];
@@ -1272,8 +1225,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const unsigned rowb = (unsigned)nx * 4u;
     const int ntiles = (nrows + S - 1) / S;
     if (prod) {
-        const unsigned vo0 = (unsigned)clampi(sxs + 2 * t, 0, nx - 1) * 4u;
-        const unsigned vo1 = (unsigned)clampi(sxs + 2 * t + 1, 0, nx - 1) * 4u;
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
         const bool lpad = padL > 0 && wv == 0;
         const bool rpad = padR > 0 && wv == ((npair - 1) >> 6);
@@ -1301,24 +1252,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
         const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
         auto rowoff = [&](int idx) { return (unsigned)clampi(y0 - RW + idx, 0, ny - 1) * rowb; };
-#if OF3D_K34PK_LD64
         // the column pair as ONE 8-byte load (dword-aligned buffer load): columns c, c + 1 when
         // both are inside the row, else the row's last two with the last one duplicated (the
         // clamped pair of the scalar form)
         const int cp = sxs + 2 * t;
         const bool dup = cp > nx - 2;
         const unsigned vp = (unsigned)(dup ? nx - 2 : cp) * 4u;
-        (void)vo0, (void)vo1;
         auto ld2 = [&](const __amdgpu_buffer_rsrc_t& r, unsigned o) {
             f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, vp, o, 0));
             if (dup) v.x = v.y;
             return v;
         };
-#else
-        auto ld2 = [&](const __amdgpu_buffer_rsrc_t& r, unsigned o) {
-            return (f2){buf_ld<float>(r, vo0, o), buf_ld<float>(r, vo1, o)};
-        };
-#endif
         f2 ring[NR], ra[PD], rb[PD];
 #pragma unroll
         for (int i = 0; i <= 2 * RW; ++i) {
@@ -1375,9 +1319,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                         }(std::make_integer_sequence<int, S / 2>{});
                         replicas(tile);
                         lds_barrier();  // tile published; the consumers are done with the other buffer
-#ifdef OF3D_K34PK_SYNC2
-                        lds_barrier();
-#endif
                         if (u0 + h0 + S >= nrows) done = true;
                     }(),
                     ...);
@@ -1418,9 +1359,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                     }
                 }
             }
-#ifdef OF3D_K34PK_SYNC2
-            lds_barrier();
-#endif
         }
     }
 }
@@ -1694,22 +1632,16 @@ constexpr int K12_TY = 4;  // rows per block
 // 168 VGPRs (one x window live at a time) and one plane per DMA chunk (LDS); and 5 % of the
 // staged columns of a 512-wide plane wasted instead of 13 %.  Same box: c3 K12 0.617 -> 0.462
 // ms, c4 4.09 -> 3.37 ms (profiles/r04/ab_k12n3/).  fp32 keeps 2 (two 8-wave blocks per CU).
-#ifndef OF3D_K12_NWX64
-#define OF3D_K12_NWX64 3
-#endif
 template <typename F>
-__host__ __device__ constexpr int k12_nwx() { return sizeof(F) == 8 ? OF3D_K12_NWX64 : 2; }
+__host__ __device__ constexpr int k12_nwx() { return sizeof(F) == 8 ? 3 : 2; }
 template <typename F>
 __host__ __device__ constexpr int k12_cw() { return 64 * k12_nwx<F>(); }
 template <typename F>
 __host__ __device__ constexpr int k12_threads() { return k12_cw<F>() * K12_TY; }
 // z passes one step late (k_grad_xyz_c) in the fp32 kernels: c5 K12 18.2-18.5 -> 17.4 ms; the
 // fp64 kernel measured slower so (c3 0.602 -> 0.645 ms, same box, profiles/r03_ab/k12_defer/)
-#ifndef OF3D_K12_DEFER
-#define OF3D_K12_DEFER 1
-#endif
 template <typename F>
-constexpr bool k12_defer() { return OF3D_K12_DEFER && sizeof(F) == 4; }
+constexpr bool k12_defer() { return sizeof(F) == 4; }
 template <typename F, int RD>
 __host__ __device__ constexpr int k12_tx() { return k12_cw<F>() - 2 * RD; }
 // LDS bytes of one staged plane: NRW rows of dt0 (CW + EPL columns) and of I (CW + EPL_T)
@@ -1731,12 +1663,9 @@ __host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * k1
 // planes per DMA chunk: 2 where two chunks of slots + the A tiles fit 80 KiB and the
 // kernel's registers allow 4 waves per SIMD (fp32 rd 3 / 6: two 8-wave blocks per CU),
 // else 3 where they fit 160 KiB, else 2
-#ifndef OF3D_K12_TWO
-#define OF3D_K12_TWO 1
-#endif
 template <typename T, typename F, int RD>
 __host__ __device__ constexpr int k12_k() {
-    if (OF3D_K12_TWO && sizeof(F) == 4 && RD <= 6 && 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 80 * 1024)
+    if (sizeof(F) == 4 && RD <= 6 && 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 80 * 1024)
         return 2;
     if (6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024) return 3;
     return 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 2 : 1;
@@ -2072,12 +2001,15 @@ __device__ __forceinline__ double cos_two_thirds_acos(double u) {
 // tools/eig_poly.py's near-degenerate, isotropic and rank-1 sets; tests/test_eig_formula.py).
 // The branch is taken by whole waves only where such tensors occur; float32-rel instances
 // never compile it.
+// It works on the scaled matrix B = (T - qI) / p (entries O(1), the caller's B11 .. B23), so the
+// cross products' squared norms neither underflow nor overflow whatever the tensor's magnitude
+// (unscaled, entries below ~1e-77 or above ~1e77 gave NaN); the caller multiplies by p.
 __device__ __forceinline__ double eigmin3_deflate(double aq, double bq, double cq, double d, double e, double f,
-                                               double p, double w) {
-    // E = T - qI (entries aq bq cq / d e f); its largest eigenvalue 2p cos(phi) with
-    // phi = (2/3) asin(u): cos(phi) = 1 - (2/9) w + O(w^2) (an error in mu only tilts the
-    // eigenvector, which moves the 2x2 block's eigenvalues at second order)
-    const double mu = 2.0 * p * (1.0 - (2.0 / 9.0) * w);
+                                               double w) {
+    // B's largest eigenvalue 2 cos(phi) with phi = (2/3) asin(u): cos(phi) = 1 - (2/9) w + O(w^2)
+    // (an error in mu only tilts the eigenvector, which moves the 2x2 block's eigenvalues at
+    // second order)
+    const double mu = 2.0 * (1.0 - (2.0 / 9.0) * w);
     const double m00 = aq - mu, m11 = bq - mu, m22 = cq - mu;
     // the eigenvector of mu: the longest cross product of two rows of E - mu I (rank 2)
     const double c0x = d * f - e * m11, c0y = e * d - m00 * f, c0z = m00 * m11 - d * d;
@@ -2142,7 +2074,7 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     // u = sqrt(w), w in [0, 1], the same way (w floored at 1e-290: u < 1e-145 reads as 0)
     const double w = fmax((1.0 - r) * 0.5, 1e-290);
     if constexpr (REFINE) {
-        if (w < 1e-6) return q + eigmin3_deflate(aq, bq, cq, d, e, f, p, w);
+        if (w < 1e-6) return q + p * eigmin3_deflate(B11, B22, B33, B12, B13, B23, w);
     }
     double iu = __builtin_amdgcn_rsq(w);
     iu = iu * (1.5 - 0.5 * w * iu * iu);
@@ -2295,14 +2227,11 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
 // windows share 2 rw W-xy planes — get ids 8 apart (same XCD, dispatched back to back) and
 // the shared planes come from that XCD's L2 instead of HBM twice.  A bijection on the grid
 // (the tail past the last whole group of 8 z-chunk sets keeps the plain order).
-#ifndef OF3D_K5C_XCD
-#define OF3D_K5C_XCD 1
-#endif
 struct K5Block {
     int bx, by, bz;
 };
 __device__ __forceinline__ K5Block k5c_block() {
-    if (!OF3D_K5C_XCD || gridDim.z == 1) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    if (gridDim.z == 1) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
     const unsigned gx = gridDim.x, gxy = gx * gridDim.y, nz = gridDim.z;
     const unsigned b = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
     const unsigned full = (gxy * nz) / (8 * nz) * (8 * nz);
@@ -2420,88 +2349,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         for (int k = 0; k <= RT0; ++k) h0[k] = k0.ht[k];
         for (size_t gi = k0g0 + threadIdx.x + (size_t)NG0 * 64 * NW; gi < k0g1; gi += 64 * NW)
             k0_group<T0, F, RT0>(k0.fr, k0.off0 + gi * V0, h0, k0.D0 + gi * V0);
-    }
-}
-// K5c for the fp32 mode on packed math: each lane carries TWO adjacent columns as one
-// float2 (v_pk_add_f32 / v_pk_mul_f32: two IEEE single ops per lane per instruction, each
-// rounded as the scalar op — bit-identical to k_wz_solve_c<float>), so a block covers 64
-// columns and the window layout in bytes is exactly the fp64 kernel's (rows of 32 8-byte
-// elements).  The solve and the eigenvalue stay per column in fp64.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <typename RelT, int RW, int NB, int R>
-__global__ __launch_bounds__(256, R == 8 ? 2 : 3) void k_wz_solve_c2(const float* __restrict__ Q, int zq0, int nz, int ny,
-                                                                   int nx, size_t fs, const float* __restrict__ hw,
-                                                                   int zo0, int nzo, float* __restrict__ vx,
-                                                                   float* __restrict__ vy, float* __restrict__ vz,
-                                                                   RelT* __restrict__ rel, int yo0) {
-    using V = f32x2;
-    constexpr int CB = 32, NW = 4, LPC = 64 / CB;  // lane-columns (2 columns each), waves, z-groups per wave
-    constexpr int ZC = NW * LPC * R;
-    constexpr int H = ZC + 2 * RW;
-    constexpr int LPR = 16;                    // lanes per window row (256 B = 64 floats)
-    constexpr int RPWI = 64 / LPR;             // window rows per wave-instruction (1 KiB)
-    constexpr int HG = (H + RPWI - 1) / RPWI;  // row groups per window
-    constexpr int NJ2 = (HG + NW - 1) / NW;    // row groups per wave
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-    V* sm = reinterpret_cast<V*>(smem_raw);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int col = lane % CB, gz = w * LPC + lane / CB;
-    const int x = blockIdx.x * 2 * CB + 2 * col;  // the lane's first column
-    const int y = yo0 + blockIdx.y;  // outputs: rows [yo0, yo0 + gridDim.y), compact layout
-    const int zc0 = zo0 + blockIdx.z * ZC;
-    const size_t ps = (size_t)ny * nx;
-    const int xc = min((int)blockIdx.x * 2 * CB + 4 * (lane % LPR), nx - 4);  // this lane's DMA floats
-    const float* qrow = Q + (size_t)y * nx + xc;
-    const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
-    V h[RW + 1];
-#pragma unroll
-    for (int k = 0; k <= RW; ++k) h[k] = (V)(hw[k]);
-    auto issue = [&](int f, int b) {
-        const float* q = qrow + f * fs;
-        const unsigned lb = lds0 + (unsigned)(b * HG * 1024);
-#pragma unroll
-        for (int j = 0; j < NJ2; ++j) {
-            const int pg = min(w + NW * j, HG - 1);
-            const int row = min(RPWI * pg + lane / LPR, H - 1);
-            const float* src = q + (size_t)(clampi(zc0 - RW + row, 0, nz - 1) - zq0) * ps;
-            glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(pg * 1024)));
-        }
-    };
-    V acc[9][R];
-#pragma unroll
-    for (int f = 0; f < NB - 1; ++f) issue(f, f);
-#pragma unroll
-    for (int f = 0; f < 9; ++f) {
-        const int ahead = min(NB - 2, 8 - f);
-        if (ahead >= 2)
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(2 * NJ2) : "memory");
-        else if (ahead == 1)
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NJ2) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
-        lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
-#pragma unroll
-        for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
-    }
-    if (x >= nx) return;
-    const int z0l = zc0 + gz * R - zo0;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        if (z0l + i >= nzo) break;
-        const size_t o = (size_t)(z0l + i) * gridDim.y * nx + (size_t)blockIdx.y * nx + x;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            if (x + e >= nx) break;
-            const double tx = acc[0][i][e], ty = acc[1][i][e], tz = acc[2][i][e], xy = acc[3][i][e],
-                         xz = acc[4][i][e], x2 = acc[5][i][e], yz = acc[6][i][e], y2 = acc[7][i][e], z2 = acc[8][i][e];
-            double ox, oy, oz;
-            solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
-            vx[o + e] = (float)ox;
-            vy[o + e] = (float)oy;
-            vz[o + e] = (float)oz;
-            rel[o + e] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
-        }
     }
 }
 constexpr int k5c_zc(int r, int nw = 4) { return 2 * nw * r; }  // output planes per K5c block (R per z-group)
@@ -2648,9 +2495,6 @@ constexpr int K1C_S = 4;
 
 // LDS-DMA K5: NB window buffers of ceil(H / RPW) 1-KB row groups (RPW = 16 B /
 // sizeof(F) rows); NJ2 = groups per wave.
-#ifndef OF3D_K5_DMA
-#define OF3D_K5_DMA 1
-#endif
 template <typename F>
 constexpr int k5_groups(int rw) {
     constexpr int rpw = 16 / (int)sizeof(F);
@@ -2658,7 +2502,6 @@ constexpr int k5_groups(int rw) {
 }
 template <typename F>
 int k5_dma_nb(int rw) {
-    if (!OF3D_K5_DMA) return 0;
     const size_t buf = (size_t)k5_groups<F>(rw) * 1024, lim = 160 * 1024;
     return 3 * buf <= lim ? 3 : (2 * buf <= lim ? 2 : 0);
 }

@@ -44,7 +44,7 @@ constexpr int kMaxChunks = 16;  // overlap mode: most z chunks per execution
 enum : unsigned {
     KU_K0C = 1u << 0, KU_K0 = 1u << 1, KU_K1C = 1u << 2, KU_K1 = 1u << 3, KU_K12 = 1u << 4, KU_K2C = 1u << 5,
     KU_K2 = 1u << 6, KU_K34 = 1u << 7, KU_K34WS = 1u << 8, KU_K3 = 1u << 9, KU_K4 = 1u << 10, KU_K5C = 1u << 11,
-    KU_K5C_PK = 1u << 12, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
+    KU_K5C_2 = 1u << 12 /* (the packed-fp32 K5c, removed) */, KU_K5DMA = 1u << 13, KU_K5 = 1u << 14, KU_SOLVE2D = 1u << 15, KU_GENERAL = 1u << 16,
     KU_K34PK = 1u << 17, KU_K5C_NEXT = 1u << 18, KU_K0M = 1u << 19,
 };
 constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy_c",    "k_grad_xy",  "k_grad_xyz_c",
@@ -53,7 +53,65 @@ constexpr const char* kKernelNames[] = {"k_tderiv_c", "k_tderiv",     "k_grad_xy
                                         "k_solve2d",  "general",      "k_prod_wyx_pk",  "k_wz_solve_c_next",
                                         "k_tderiv_multi"};
 
+// Kernel-family switches, read from the environment once per plan (at of3d_plan_create; the
+// host entry's plan cache keys on them too).  The defaults are the product; the tests force each
+// family in turn to check that every one gives the same bits (INTEGRATION.md §5 lists them).
+struct Knobs {
+    bool k0c = true;      // OF3D_K0C=0: runtime-radius K0 instead of the compile-time one
+    bool k1c = true;      // OF3D_K1C=0: k_grad_xy instead of the column-march K1c
+    bool k2c = true;      // OF3D_K2C=0: k_grad_z instead of the z-march K2c
+    int k12 = -1;         // OF3D_K12: 0 off, 1 forced, -1 by volume size
+    int k12_zc = 0;       // OF3D_K12_ZC: forced K12 march length (planes; 0: by volume size)
+    bool k34 = true;      // OF3D_K34=0: K3 + K4 instead of the fused K34
+    int k34_uq = -1;      // OF3D_K34_UQ: 0 duplicate staging, 1 unique, 2 wave-specialised, 3 packed fp32 only
+    bool k34_ws = true;   // OF3D_K34_WS=0: no wave-specialised candidates
+    bool k34_pk = true;   // OF3D_K34_PK=0: no packed-fp32 candidates
+    int k34_cand = -1;    // OF3D_K34_CAND=i: pin candidate i (no autotune)
+    bool k34_strict = false;  // OF3D_K34_CAND_STRICT=1: a pin past the candidates fails
+    bool k34_tune = true;     // OF3D_K34_TUNE=0: the heuristic pick, untimed
+    bool k5c = true;      // OF3D_K5C=0: k_wz_solve_dma / k_wz_solve instead of K5c
+    int k5c_r = 8;        // OF3D_K5C_R=4: 32-plane K5c blocks
+    int k5c_nw = 4;       // OF3D_K5C_NW=8: 8-wave, 128-plane K5c blocks
+    bool pipe = true;     // OF3D_PIPE=0: no next-frame K0 inside K5c
+    bool general = false;  // OF3D_GENERAL=1: the general-radius path
+    int64_t zchunk = 0;   // OF3D_ZCHUNK: overlap mode's z chunk (planes; 0 serial)
+    int verbose = 0;      // OF3D_VERBOSE: plan choices on stderr
+    static Knobs read() {
+        Knobs k;
+        auto iv = [](const char* name, long dflt) {
+            const char* e = getenv(name);
+            return (e && e[0]) ? atol(e) : dflt;
+        };
+        k.k0c = iv("OF3D_K0C", 1) != 0;
+        k.k1c = iv("OF3D_K1C", 1) != 0;
+        k.k2c = iv("OF3D_K2C", 1) != 0;
+        k.k12 = (int)iv("OF3D_K12", -1);
+        k.k12_zc = (int)iv("OF3D_K12_ZC", 0);
+        k.k34 = iv("OF3D_K34", 1) != 0;
+        k.k34_uq = (int)iv("OF3D_K34_UQ", -1);
+        k.k34_ws = iv("OF3D_K34_WS", 1) != 0;
+        k.k34_pk = iv("OF3D_K34_PK", 1) != 0;
+        k.k34_cand = (int)iv("OF3D_K34_CAND", -1);
+        k.k34_strict = iv("OF3D_K34_CAND_STRICT", 0) == 1;
+        k.k34_tune = iv("OF3D_K34_TUNE", 1) != 0;
+        k.k5c = iv("OF3D_K5C", 1) != 0;
+        k.k5c_r = iv("OF3D_K5C_R", 8) == 4 ? 4 : 8;
+        k.k5c_nw = iv("OF3D_K5C_NW", 4) == 8 ? 8 : 4;
+        k.pipe = iv("OF3D_PIPE", 1) != 0;
+        k.general = iv("OF3D_GENERAL", 0) == 1;
+        k.zchunk = std::max(0L, iv("OF3D_ZCHUNK", 0));
+        k.verbose = (int)iv("OF3D_VERBOSE", 0);
+        return k;
+    }
+    auto tie() const {
+        return std::tie(k0c, k1c, k2c, k12, k12_zc, k34, k34_uq, k34_ws, k34_pk, k34_cand, k34_strict, k34_tune, k5c,
+                        k5c_r, k5c_nw, pipe, general, zchunk, verbose);
+    }
+    bool operator==(const Knobs& o) const { return tie() == o.tie(); }
+};
+
 struct of3d_plan {
+    Knobs kn;  // read at creation
     int ndim = 3;
     bool rel64 = false;  // OF3D_REL_F64
     bool fp32 = false;   // OF3D_FP32: passes in float
@@ -71,15 +129,11 @@ struct of3d_plan {
     size_t k1_lds = 0, k2_lds = 0, k3_lds = 0, k4_lds = 0, k5_lds = 0;
     int k5_nb = 0;       // LDS-DMA K5 buffers (0: register-staged K5)
     size_t k5d_lds = 0;
-    bool k1c = true;  // column-march K1 where instantiated (OF3D_K1C=0: k_grad_xy)
-    bool k2c = true;  // z-march K2 where instantiated (OF3D_K2C=0: k_grad_z)
-    bool k12 = true;  // fused gradient kernel where instantiated (OF3D_K12=0: K1c + K2c)
     bool general = false;  // radii beyond the tiled kernels' limits: the general-radius path
     // K5c (compile-time-radius W z + solve); nullptr: k_wz_solve_dma / k_wz_solve
     const void* k5c = nullptr;
     size_t k5c_lds = 0;
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
-    bool k5c_pk = false;  // packed-fp32 K5c (64 columns per block)
     const void* k5c_next = nullptr;  // K5c that also forms the next frame's dt0 (frame pipelining)
     // frame pipelining (of3d_plan_execute_next): the dt0 a previous call formed for these frames
     bool pipe_valid = false;
@@ -235,15 +289,14 @@ template <typename F>
 int k34_setup(of3d_plan* p, int np) {
     p->k34 = {};
     p->k34_cand.clear();
-    if (const char* e = getenv("OF3D_K34"); e && e[0] == '0') return 0;
+    const Knobs& kn = p->kn;
+    if (!kn.k34) return 0;
     const int rw = p->rw, nx = (int)p->nx;
     const size_t es = sizeof(F);
     if ((size_t)p->ny * p->nx * es > 0x7fffffffu) return 0;  // 32-bit buffer offsets within a plane
     long best_lanes = 0;
     int best_waves = 0;
-    const char* env_nw = getenv("OF3D_K34_NW");  // overrides (experiments)
-    const char* env_s = getenv("OF3D_K34_S");
-    const char* env_uq = getenv("OF3D_K34_UQ");  // 0: duplicate staging only, 1: unique only (2: specialised only)
+    const int uq = kn.k34_uq;  // 0: duplicate staging only, 1: unique only (2: specialised, 3: packed fp32 only)
     auto occupancy = [&](const void* fn, int cw, size_t lds, int& waves) -> int {
         OF3D_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         int nb = 0;
@@ -252,12 +305,9 @@ int k34_setup(of3d_plan* p, int np) {
         return 0;
     };
     for (int s : {16, 8, 4}) {
-        if (env_s && atoi(env_s) != s) continue;
-        const void* fd = (env_uq && env_uq[0] == '1') ? nullptr
-                                                       : (np == 9 ? k34_fn<F, 9>(rw, s, 4) : k34_fn<F, 5>(rw, s, 4));
-        const void* fu = (env_uq && env_uq[0] == '0') ? nullptr : (np == 9 ? k34_fn_uq<F, 9>(rw, s) : k34_fn_uq<F, 5>(rw, s));
+        const void* fd = uq == 1 ? nullptr : (np == 9 ? k34_fn<F, 9>(rw, s, 4) : k34_fn<F, 5>(rw, s, 4));
+        const void* fu = uq == 0 ? nullptr : (np == 9 ? k34_fn_uq<F, 9>(rw, s) : k34_fn_uq<F, 5>(rw, s));
         for (int nw : {1, 2, 3, 4, 8}) {  // launch bound 512
-            if (env_nw && atoi(env_nw) != nw) continue;
             const int cw = 64 * nw;
             if (fd && nw <= 4) {  // duplicate staging
                 const int tx = (cw - 2 * rw) & ~3;  // whole phase-B items
@@ -299,13 +349,15 @@ int k34_setup(of3d_plan* p, int np) {
                     if (lds <= 160 * 1024 && !occupancy(fu, cw, lds, waves) && waves >= nw)
                         p->k34_cand.push_back({fu, cw, s, tx, nbx, lds});
                     // the wave-specialised form of the same geometry (8 producer + 8 consumer waves)
-                    const void* fw = nw == 8 ? (np == 9 ? k34_fn_ws<F, 9>(rw, s) : k34_fn_ws<F, 5>(rw, s)) : nullptr;
+                    const void* fw =
+                (nw == 8 && kn.k34_ws) ? (np == 9 ? k34_fn_ws<F, 9>(rw, s) : k34_fn_ws<F, 5>(rw, s)) : nullptr;
                     int wsw = 0;
                     if (fw && lds <= 160 * 1024 && !occupancy(fw, 2 * cw, lds, wsw) && wsw >= 2 * nw)
                         p->k34_cand.push_back({fw, cw, s, tx, nbx, lds, 2 * cw});
                     // fp32: the packed form (column pairs / row pairs on float2, 8-wave blocks)
                     if constexpr (sizeof(F) == 4) {
-                        const void* fp = nw == 8 ? (np == 9 ? k34_fn_pk<9>(rw, s) : k34_fn_pk<5>(rw, s)) : nullptr;
+                        const void* fp =
+                            (nw == 8 && kn.k34_pk) ? (np == 9 ? k34_fn_pk<9>(rw, s) : k34_fn_pk<5>(rw, s)) : nullptr;
                         const size_t lpk = (size_t)s * k34_pitch(std::min(tx, nx), rw) * 8;
                         int pkw = 0;
                         if (fp && lpk <= 160 * 1024 && !occupancy(fp, cw, lpk, pkw) && pkw >= nw)
@@ -315,10 +367,10 @@ int k34_setup(of3d_plan* p, int np) {
             }
         }
     }
-    if (env_uq && (env_uq[0] == '2' || env_uq[0] == '3')) {  // tests: wave-specialised (3: packed fp32) only
+    if (uq == 2 || uq == 3) {  // tests: wave-specialised (3: packed fp32) only
         std::vector<of3d_plan::K34Geom> ws;
         for (const auto& k : p->k34_cand)
-            if (k.nthr && (env_uq[0] == '2' || k.nthr == k.cw)) ws.push_back(k);
+            if (k.nthr && (uq == 2 || k.nthr == k.cw)) ws.push_back(k);
         p->k34_cand = ws;
         p->k34 = ws.empty() ? of3d_plan::K34Geom{} : ws.front();
     }
@@ -327,7 +379,7 @@ int k34_setup(of3d_plan* p, int np) {
         OF3D_HIP(hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (p->k34.fn)
         OF3D_HIP(hipFuncSetAttribute(p->k34.fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if (getenv("OF3D_VERBOSE") && p->k34.fn)
+    if (kn.verbose && p->k34.fn)
         fprintf(stderr, "of3d: K34 cw=%d s=%d tx=%d nbx=%d lds=%zu lanes=%ld waves/CU=%d\n", p->k34.cw, p->k34.s,
                 p->k34.tx, p->k34.nbx, p->k34.lds, best_lanes, best_waves);
     return 0;
@@ -338,38 +390,19 @@ template <typename F>
 int k5c_setup(of3d_plan* p) {
     p->k5c = nullptr;
     p->k5c_next = nullptr;
-    p->k5c_pk = false;
     p->k5c_nw = 4;
-    if (const char* e = getenv("OF3D_K5C"); e && e[0] == '0') return 0;
+    if (!p->kn.k5c) return 0;
     if (p->ndim != 3 || p->nx % (16 / (int)sizeof(F))) return 0;  // 16-byte DMA rows
-    const char* er = getenv("OF3D_K5C_R");
-    // planes per z-group: 8 (64-plane blocks) or 4 (32).  A 128-plane fp32 instance (R 16, 4 waves,
-    // 191 VGPRs, two blocks per CU) measured slower: c5 fp32 41.8 vs 39.7 ms, c3 fp32 0.74 vs 0.68
-    int r = er ? atoi(er) : 8;
-    // 6 planes (48-plane blocks, 160 VGPRs: three blocks per CU) measured slower: c3 K5c 1.00 ->
-    // 1.05 ms, c4 7.17 -> 7.30, c5 fp32 34.7 -> 35.8 (profiles/r04/ab_k5r6/)
-    if (r != 4) r = 8;  // the instances compiled (k5c_fn): the launch grid must match them
-    // fp32: the packed kernel (two columns per lane as float2; window bytes as the fp64 kernel's)
-    const void* pk = nullptr;
-    if constexpr (sizeof(F) == 4) {
-        const size_t buf2 = (size_t)k5c_groups<double>(p->rw, r) * 1024;
-        const int nb2 = 2 * 3 * buf2 <= 160 * 1024 ? 3 : 2;
-        pk = p->rel64 ? k5c2_fn<double>(p->rw, nb2, r) : k5c2_fn<float>(p->rw, nb2, r);
-        if (pk) {
-            p->k5c_r = r;
-            p->k5c_lds = nb2 * buf2;
-            p->k5c_pk = true;
-            OF3D_HIP(hipFuncSetAttribute(pk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
-            p->k5c = pk;
-            return 0;
-        }
-    }
+    // planes per z-group: 8 (64-plane blocks) or 4 (32; OF3D_K5C_R=4), the compiled instances
+    // (k5c_fn).  A 128-plane fp32 instance (R 16, 191 VGPRs) measured slower (c5 fp32 41.8 vs
+    // 39.7 ms), so did 6 planes (48-plane blocks, three per CU: c3 K5c 1.00 -> 1.05 ms,
+    // profiles/r04/ab_k5r6/) and the packed-fp32 K5c (float2 lanes: c5 36.5 vs 34.5 ms, round 4,
+    // profiles/r04/ab_k5c_fp32/; removed in round 5)
+    int r = p->kn.k5c_r;
     // OF3D_K5C_NW=8: 8-wave blocks of 128 output planes (window 1.33x the outputs instead of
     // 1.66x; one block per CU) — bit-identical but measured no faster (c3 1.118 vs 1.121 ms,
     // c4 8.54 vs 7.90, c5 fp32 43.6 vs 40.4): K5c is not bound by its window re-reads
-    const char* enw = getenv("OF3D_K5C_NW");
-    int nw = enw ? atoi(enw) : 4;
-    if (nw != 8) nw = 4;
+    int nw = p->kn.k5c_nw;
     if (nw == 8) r = 8;  // the 8-wave instances are R 8 only (k5c_fn): grid and LDS follow r
     size_t buf = (size_t)k5c_groups<F>(p->rw, r, nw) * 1024;
     int nb = nw == 8 ? (3 * buf <= 160 * 1024 ? 3 : 0) : (2 * 3 * buf <= 160 * 1024 ? 3 : 2);  // 4 waves: two blocks per CU
@@ -388,7 +421,7 @@ int k5c_setup(of3d_plan* p) {
     p->k5c = fn;
     // the same geometry with the next frame's K0 after the solve (uint16 frames; OF3D_PIPE=0: off)
     p->k5c_next = nullptr;
-    if (const char* e = getenv("OF3D_PIPE"); !(e && e[0] == '0')) {
+    if (p->kn.pipe) {
         const void* fx = p->rel64 ? k5c_fn<F, double>(p->rw, nb, r, nw, p->rt) : k5c_fn<F, float>(p->rw, nb, r, nw, p->rt);
         if (fx) {
             OF3D_HIP(hipFuncSetAttribute(fx, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p->k5c_lds));
@@ -407,31 +440,11 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     if (yb1 < 0) yb1 = ny;
     const int nyo = yb1 - yb0;  // output rows (row-slab plans: the rank's own rows)
     int tx = k.tx, nbx = k.nbx;
-    // chunk-major order (k34_block, cpg < 0): the 9 products of a row chunk read the same four
-    // gradient rows, which stay in an XCD's L2 only while the chunk's blocks run together — c5's
-    // 79 GB of K34 reads per launch for 34 GB of gradients (planes of 32 MiB of gradient rows).
-    // Off by default: chunks of OF3D_K34_CM rows measured slower (c3 1.63 -> 1.66 / 1.71 / 1.85
-    // ms at 256 / 128 / 64 rows, c5 fp32 46.0 -> 48.5 / 50.3 ms at 128 / 64, c4 11.58 -> 11.37 /
-    // 11.59 / 11.82 at 256 / 128 / 64; profiles/r04/ab_k34_cm.txt): the re-formed halo rows of
-    // every chunk cost more than the L2 misses, which K34 (VALU-bound) mostly hides.
-    const char* ecm = getenv("OF3D_K34_CM");
-    const int cm_rows = ecm ? atoi(ecm) : 0;
-    if (cm_rows > 0 && nyo >= 2 * cm_rows) {
-        int nyc = (cm_rows + k.s - 1) / k.s * k.s;
-        const int nyb = (nyo + nyc - 1) / nyc;
-        int cpg = -1, groups = ng;
-        const int mb = nf * nbx;
-        const unsigned blocks = (unsigned)(8 * ((ng + 7) / 8) * nyb * mb);
-        void* args[] = {(void*)&G,   (void*)&P,   (void*)&ny,  (void*)&nx,  (void*)&fs,     (void*)&hw,  (void*)&tx,
-                        (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1};
-        return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);
-    }
     const int nyb_max = std::max(1, nyo / 32);
     // block target 2048: longer row chunks re-read fewer halo rows (c3 wave-specialised K34 1.67
     // vs 1.76 ms at 4096, 1.73 at 1024; c2 lockstep K34 0.175 vs 0.191 ms, frame 0.420 vs 0.435;
-    // c4 neutral).  OF3D_K34_NYBX scales it (experiments).
-    static const double tscale = getenv("OF3D_K34_NYBX") ? atof(getenv("OF3D_K34_NYBX")) : 1.0;
-    const long target = std::max(1L, (long)(2048.0 * tscale));
+    // c4 neutral).  (A chunk-major block order for L2 reuse measured slower: round 4.)
+    const long target = 2048;
     int nyb = 1;
     while (nyb < nyb_max && (long)ng * nyb * nf * k.nbx < target) ++nyb;
     int nyc = (nyo + nyb - 1) / nyb;
@@ -515,10 +528,10 @@ int k34_tune(of3d_plan* p) {
     if (!(ms[bi] < 0.97f * ms[0])) bi = 0;
     const float best = ms[bi];
     p->k34 = p->k34_cand[bi];
-    if (getenv("OF3D_VERBOSE"))
+    if (p->kn.verbose)
         fprintf(stderr, "of3d: K34 tuned over %zu shapes: cand=%zu cw=%d s=%d tx=%d nbx=%d thr=%d lds=%zu (%.3f ms)\n",
                 p->k34_cand.size(), bi, p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx, p->k34.nthr, p->k34.lds, best);
-    if (getenv("OF3D_VERBOSE") && atoi(getenv("OF3D_VERBOSE")) > 1)
+    if (p->kn.verbose > 1)
         for (size_t i = 0; i < nc; ++i)
             fprintf(stderr, "of3d:   K34 cand %zu: cw=%d s=%d tx=%d thr=%d lds=%zu %.3f ms\n", i, p->k34_cand[i].cw,
                     p->k34_cand[i].s, p->k34_cand[i].tx, p->k34_cand[i].nthr, p->k34_cand[i].lds, ms[i]);
@@ -553,9 +566,6 @@ int set_attrs_t(of3d_plan* p) {
               attr(k5_dma_kernel<F, double>(p->rw, p->k5_nb), p->k5d_lds);
     }
     if (rc) return -1;
-    if (const char* e = getenv("OF3D_K1C"); e && e[0] == '0') p->k1c = false;
-    if (const char* e = getenv("OF3D_K2C"); e && e[0] == '0') p->k2c = false;
-    if (const char* e = getenv("OF3D_K12"); e && e[0] == '0') p->k12 = false;
     for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32}) {
         if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
             OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -570,7 +580,7 @@ int set_attrs_t(of3d_plan* p) {
 // tile at most 160 KiB of LDS, kMaxR for the tap padding) run the general-radius path
 // (k_corr_gen passes: the same arithmetic, any radius).  OF3D_GENERAL=1 forces it (tests).
 bool needs_general(const of3d_plan* p) {
-    if (const char* e = getenv("OF3D_GENERAL"); e && e[0] == '1') return true;
+    if (p->kn.general) return true;
     if (p->rd > 24 || p->rs > kMaxR || p->rw > kMaxR) return true;
     const size_t e = p->fp32 ? 4 : 8, lim = 160 * 1024;
     const size_t k3 = (size_t)(K3_STEP + 2 * p->rw) * 64 * e;
@@ -791,13 +801,12 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     // K12 pays where its blocks can march >= 32 planes and still fill the GPU (c2, 256^2 x 64:
     // 16-plane marches re-form 12 halo planes each, K1c + K2c measured faster; c3: K12 0.62 vs
     // 0.83 ms); OF3D_K12=1 forces it, OF3D_K12=0 disables it
-    const char* k12_env = getenv("OF3D_K12");
     const int k12_tiles = (int)cdiv(nx, k12_cw<F>() - 2 * p->rd) * (int)cdiv(ny, K12_TY);
     const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
     // (fp32 plans, rd <= 6: two blocks per CU — c3 0.27 + 0.36 ms vs K1c + K2c 0.43 + 0.25, c5
     // 12.7 + 21.3 vs 23.5 + 13.2; rd 9 in fp32 runs one block per CU: K1c + K2c)
-    const void* k12 = (d3 && p->k12 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
-                       ((k12_big && (sizeof(F) == 8 || p->rd <= 6)) || (k12_env && k12_env[0] == '1')))
+    const void* k12 = (d3 && p->kn.k12 != 0 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
+                       ((k12_big && (sizeof(F) == 8 || p->rd <= 6)) || p->kn.k12 == 1))
                           ? k12_fn<F>(dtype, p->rd, p->rs) : nullptr;
     // K0 batching (of3d_plan_execute_ahead, `ahead` >= 0 frames past the window in d_frames):
     // this call's dt0 from a slot an earlier call formed for exactly this window, else one
@@ -873,7 +882,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                 size_t ng = n / V;
                 const unsigned blocks = (unsigned)std::min<size_t>((ng + 255) / 256, 256 * 32);
                 void* args[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&rt_arg, (void*)&tp.t, (void*)&D0};
-                const void* k0 = k0c_fn<F>(dtype, p->rt);
+                const void* k0 = p->kn.k0c ? k0c_fn<F>(dtype, p->rt) : nullptr;
                 if (k0) {
                     void* cargs[] = {(void*)&fr, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0};
                     OF3D_HIP(hipLaunchKernel(k0, dim3(blocks), dim3(256), cargs, 0, st));
@@ -900,15 +909,13 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&ny, (void*)&nx, (void*)&nb_arg, (void*)&tp,
                         (void*)&Bo, (void*)&fs, (void*)&need_b4};
         // (32-bit buffer offsets within a plane: planes up to 2 GiB)
-        const bool k1c_ok = p->k1c && plane * sizeof(F) <= 0x7fffffffu;
+        const bool k1c_ok = p->kn.k1c && plane * sizeof(F) <= 0x7fffffffu;
         const void* k1c = k1c_ok ? k1c_fn<F>(dtype, p->rd, p->rs) : nullptr;
         if (k1c) {
             // column march: 128-column blocks up to nx 256, else 256; rows in chunks of >= 32
-            static const int cw_env = getenv("OF3D_K1C_CW") ? atoi(getenv("OF3D_K1C_CW")) : 0;  // experiments
-            static const int nyc_env = getenv("OF3D_K1C_NYC") ? atoi(getenv("OF3D_K1C_NYC")) : 32;
-            const int cw = cw_env ? cw_env : (nx <= 256 ? 128 : 256);  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
+            const int cw = nx <= 256 ? 128 : 256;  // c2: 128 (86 vs 98 us), c3: 256 (0.65 vs 0.69 ms)
             int tx = (cw - 2 * p->rd) & ~3, nbx = (nx + tx - 1) / tx;
-            int nyc = std::min(ny, nyc_env), nyb;
+            int nyc = std::min(ny, 32), nyb;
             while (true) {
                 nyc = (nyc + K1C_S - 1) / K1C_S * K1C_S;
                 nyb = (ny + nyc - 1) / nyc;
@@ -941,8 +948,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             // planes per block: the longest march (up to 256) that still gives >= 1024 blocks
             // (each march re-forms 2 rd halo planes), at least 16.  Measured: c5 fp32 K12 20.7 /
             // 20.0 / 19.7 ms at 64 / 128 / 256, c4 fp64 4.40 / 4.12 at 64 / 128; c3 keeps 64
-            const char* zc_env = getenv("OF3D_K12_ZC");  // forced march length (tests, experiments)
-            int zc = zc_env ? atoi(zc_env) : 0;
+            int zc = p->kn.k12_zc;  // OF3D_K12_ZC: forced march length (tests)
             if (zc <= 0) {
                 zc = 256;
                 // (three full rounds of one block per CU for the 12-wave fp64 blocks)
@@ -959,7 +965,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             return 0;
         }
         const void* k2c = nullptr;
-        if (p->k2c) {
+        if (p->kn.k2c) {
             if (p->rd == 6 && p->rs == 2) k2c = (const void*)k_grad_z_c<F, 6, 2>;
             if (p->rd == 3 && p->rs == 1) k2c = (const void*)k_grad_z_c<F, 3, 1>;
         }
@@ -1038,13 +1044,13 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&tp.wr, (void*)&rw_arg, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy,
                             (void*)&ovz, (void*)&orel};
             if (p->k5c) {
-                dim3 gc(cdiv(nx, p->k5c_pk ? 64 : 32), (unsigned)(p->yb - p->ya), cdiv(no, k5c_zc(p->k5c_r, p->k5c_nw)));
+                dim3 gc(cdiv(nx, 32), (unsigned)(p->yb - p->ya), cdiv(no, k5c_zc(p->k5c_r, p->k5c_nw)));
                 int yo0 = (int)p->ya;
                 void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny,  (void*)&nx,  (void*)&fs,
                                  (void*)&tp.w, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz,
                                  (void*)&orel, (void*)&yo0, (void*)&k0n};
                 OF3D_HIP(hipLaunchKernel(fuse_next ? p->k5c_next : p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
-                p->used |= fuse_next ? KU_K5C_NEXT : (p->k5c_pk ? KU_K5C_PK : KU_K5C);
+                p->used |= fuse_next ? KU_K5C_NEXT : KU_K5C;
             } else if (p->k5_nb) {
                 const void* k = p->rel64 ? k5_dma_kernel<F, double>(p->rw, p->k5_nb) : k5_dma_kernel<F, float>(p->rw, p->k5_nb);
                 OF3D_HIP(hipLaunchKernel(k, g, dim3(64, kg.g), args, p->k5d_lds, st));
@@ -1195,6 +1201,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
         of3d_plan* operator->() const { return p; }
         of3d_plan* release() { of3d_plan* q = p; p = nullptr; return q; }
     } p;
+    p->kn = Knobs::read();
     p->ndim = ndim;
     p->rel64 = (mode & OF3D_REL_F64) != 0;
     p->fp32 = (mode & OF3D_FP32) != 0;
@@ -1225,20 +1232,19 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     OF3D_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
     OF3D_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
     for (auto& e : p->ev_chunk) OF3D_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (const char* e = getenv("OF3D_ZCHUNK")) p->zchunk = atoll(e);
+    p->zchunk = p->kn.zchunk;
     // OF3D_K34_CAND=i pins the i-th candidate geometry of the K34 autotune (tests run every
     // candidate and compare bits; multi-rank runs can pin one choice for every rank)
-    if (const char* e = getenv("OF3D_K34_CAND"); e && e[0]) {
-        const size_t i = (size_t)atoll(e);
+    if (p->kn.k34_cand >= 0) {
+        const size_t i = (size_t)p->kn.k34_cand;
         if (i < p->k34_cand.size()) {
             p->k34 = p->k34_cand[i];
         } else {  // a pin meant for another plan shape (fewer candidates): keep the heuristic pick
-            const char* st = getenv("OF3D_K34_CAND_STRICT");
-            if (st && st[0] == '1') return fail("of3d: OF3D_K34_CAND out of range");
+            if (p->kn.k34_strict) return fail("of3d: OF3D_K34_CAND out of range");
             fprintf(stderr, "of3d: OF3D_K34_CAND=%zu ignored for this plan (%zu candidates)\n", i,
                     p->k34_cand.size());
         }
-    } else if (const char* e = getenv("OF3D_K34_TUNE"); !(e && e[0] == '0')) {
+    } else if (p->kn.k34_tune) {
         OF3D_HIP(hipMemsetAsync(p->X, 0, 9 * p->fs * es, p->stream));  // defined (zero) tuning inputs
         OF3D_HIP(hipMemsetAsync(p->Y, 0, 9 * p->fs * es, p->stream));
         if ((p->fp32 ? k34_tune<float>(p.get()) : k34_tune<double>(p.get()))) return -1;
@@ -1279,9 +1285,10 @@ struct CacheKey {
     int64_t nz, ny, nx;
     std::vector<double> taps;
     std::vector<int> radii;
+    Knobs kn;  // a plan made under other kernel-family switches is another plan
     bool operator==(const CacheKey& o) const {
         return ndim == o.ndim && device == o.device && mode == o.mode && nz == o.nz && ny == o.ny && nx == o.nx && taps == o.taps &&
-               radii == o.radii;
+               radii == o.radii && kn == o.kn;
     }
 };
 
@@ -1293,7 +1300,7 @@ struct CacheEntry {
 std::vector<CacheEntry> g_cache;  // small LRU
 
 CacheKey make_key(int ndim, int device, int mode, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* t) {
-    CacheKey k{ndim, device, mode, nz, ny, nx, {}, {t->rd, t->rs, t->rt, t->rw}};
+    CacheKey k{ndim, device, mode, nz, ny, nx, {}, {t->rd, t->rs, t->rt, t->rw}, Knobs::read()};
     auto add = [&](const double* w, int r) { k.taps.insert(k.taps.end(), w, w + 2 * r + 1); };
     add(t->gauss, t->rd);
     add(t->deriv, t->rd);

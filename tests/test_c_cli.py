@@ -32,6 +32,32 @@ def test_cli_usage_error(cli):
     assert r.returncode == 2 and "usage" in r.stderr
 
 
+def test_cli_rejects_bad_taps_header_and_pipes(cli, tmp_path):
+    """Malformed inputs fail with status 2 before any pointer arithmetic or device call: a
+    negative / fractional tap radius, a taps file whose size does not match its radii, an input
+    that cannot be sized (a FIFO), bad dimensions."""
+    img = tmp_path / "img.u16"
+    np.zeros((7, 2, 8, 8), np.uint16).tofile(img)
+    for hdr in ([-5, 1, 1, 3], [2.5, 1, 1, 3], [2, 1, 40, 3], [1e9, 1, 1, 3]):
+        tp = tmp_path / "bad.f64"
+        np.array(hdr + [0.0] * 64, np.float64).tofile(tp)
+        r = subprocess.run([cli, str(img), "7", "2", "8", "8", str(tp), str(tmp_path / "o_")],
+                           capture_output=True, text=True)
+        assert r.returncode == 2 and "bad tap radius" in r.stderr, (hdr, r.stderr)
+    tp = tmp_path / "short.f64"
+    np.array([1, 1, 1, 1] + [0.0] * 3, np.float64).tofile(tp)
+    r = subprocess.run([cli, str(img), "7", "2", "8", "8", str(tp), str(tmp_path / "o_")], capture_output=True, text=True)
+    assert r.returncode == 2 and "does not match" in r.stderr
+    # the image through a pipe (/dev/stdin): ftell cannot size it -> refused, no overrun
+    good = tmp_path / "good.f64"
+    _taps_file(good, 1, 1, 1)
+    r = subprocess.run([cli, "/dev/stdin", "7", "2", "8", "8", str(good), str(tmp_path / "o_")],
+                       input=np.zeros(7 * 2 * 8 * 8, np.uint16).tobytes(), capture_output=True)
+    assert r.returncode == 2 and b"bad input files" in r.stderr
+    r = subprocess.run([cli, str(img), "7", "0", "8", "8", str(tp), str(tmp_path / "o_")], capture_output=True, text=True)
+    assert r.returncode == 2 and "bad dimensions" in r.stderr
+
+
 def _taps_file(path, s, t, w):
     from opticalflow3d_dev_amd import make_taps, radii
 

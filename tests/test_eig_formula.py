@@ -39,6 +39,17 @@ def test_refined_formula_meets_fp64_tolerance(coef, psd):
     assert err32.max() > TOL_FP64
 
 
+def test_refined_formula_extreme_magnitudes(coef):
+    """Tensors of magnitude 1e-100 and 1e100 (every hard set): the deflation works on the
+    scaled matrix, so nothing under- or overflows — still 1e-12 lambda_max, no NaN."""
+    args, ref = eig_poly.test_set(n=60000, seed=11, extreme=True)
+    lmax = np.abs(ref).max(axis=1)
+    got = eig_poly.eigmin3(*args, m=coef, refine=True)
+    assert np.isfinite(got).all()
+    err = np.abs(got - ref[:, 0]) / lmax
+    assert err.max() <= 1e-12, err.max()
+
+
 def test_polynomial_matches_acos(coef):
     u = np.linspace(0, 1, 100001)
     assert np.abs(eig_poly.horner(coef, 2 * u - 1) - np.cos(2 / 3 * np.arccos(u))).max() < 5e-15

@@ -193,7 +193,7 @@ def test_c3_fp32_plans_vs_oracle_and_candidates(c3):
     mode = _lib.OF3D_FP32
     ref, _ = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
     ncand = k34_candidates(d_in, p, mode)
-    for v in [dict(OF3D_K34_CAND=i) for i in range(ncand)] + [dict(OF3D_K12=0), dict(OF3D_K5C_PK=1)]:
+    for v in [dict(OF3D_K34_CAND=i) for i in range(ncand)] + [dict(OF3D_K12=0), dict(OF3D_K5C_R=4)]:
         with env(**v):
             outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
         for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
@@ -301,26 +301,6 @@ def test_c5_shaped_fp32_plan_candidates_and_oracle():
     assert "k_prod_wyx_pk" in seen, seen
     crop_check(host_in, ref, (16, 32, 24, 40, 1016, 1040), p["s"], p["t"], p["w"], fp32=True)
     crop_check(host_in, ref, (32, 48, 44, 64, 2020, 2048), p["s"], p["t"], p["w"], fp32=True)
-
-
-@pytest.mark.parametrize("mode,cm", [(0, 8), (0, 16), ("fp32", 8)])
-def test_k34_chunk_major_order_bit_identical(long_volume, mode, cm):
-    """K34's chunk-major block order (OF3D_K34_CM: row chunks of cm rows, each XCD running its
-    planes' chunks one after another; an opt-in L2 experiment) on the 320-plane volume: every
-    K34 candidate bit-identical to the plane-major order, fp64 and fp32."""
-    from opticalflow3d_dev_amd import _lib
-
-    d_in, _ = long_volume
-    p = LONG
-    m = _lib.OF3D_FP32 if mode == "fp32" else 0
-    with env(OF3D_K34_CM=0):
-        ref, _ = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=m)
-        ncand = k34_candidates(d_in, p, m)
-    for i in range(ncand):
-        with env(OF3D_K34_CM=cm, OF3D_K34_CAND=i):
-            outs, ks = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=m)
-        for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):
-            assert same_bits(a, b), (cm, i, name, ks)
 
 
 C4S = dict(nt=13, nz=24, ny=64, nx=1024, s=2, t=2, w=5)

@@ -14,7 +14,7 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_PK", "OF3D_K5C_NW", "OF3D_K34_UQ")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_NW", "OF3D_K34_UQ")
 
 
 def _run(img, s, t, w, ndim, mode, old, force=None, kernels=None):
@@ -95,18 +95,6 @@ def test_fused_gradients_k12_forced(case, fp32):
     mode = _lib.OF3D_FP32 if fp32 else 0
     new = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_K12": "1"})
     ref = _run(img, s, t, w, ndim, mode, old=True)
-    for a, b in zip(new, ref):
-        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
-
-
-@pytest.mark.parametrize("case", range(3))
-def test_packed_fp32_wz_solve(case):
-    """The packed-fp32 K5c (OF3D_K5C_PK=1, float2 lanes: v_pk_add/mul_f32) against the
-    older fp32 kernels: bit-identical."""
-    shape, (s, t, w), ndim = CASES[case]
-    img = np.random.default_rng(500 + case).integers(0, 4096, size=shape).astype(np.uint16)
-    new = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=False, force={"OF3D_K5C_PK": "1"})
-    ref = _run(img, s, t, w, ndim, _lib.OF3D_FP32, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
 

@@ -233,3 +233,14 @@ def test_rel3d_device_formula_near_degenerate(psd):
         assert err.max() <= tol, (f64, err.max())
         if f64:
             assert err.max() <= 1e-12, err.max()
+    # fp64 rel on tensors of magnitude 1e-100 / 1e100 too (the deflation on the scaled matrix:
+    # no under- or overflow; float32 rel cannot hold such values)
+    args, ref = eig_poly.test_set(n=60000, seed=13, psd=psd, extreme=True)
+    lmax = np.abs(ref).max(axis=1)
+    t = torch.from_numpy(np.ascontiguousarray(np.stack(args))).to(dev)
+    out = torch.empty(len(lmax), dtype=torch.float64, device=dev)
+    _lib.check(lib.of3d_rel3d(t.data_ptr(), len(lmax), out.data_ptr(), 1, s))
+    torch.cuda.synchronize(dev)
+    got = out.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert (np.abs(got - ref[:, 0]) / lmax).max() <= 1e-12

@@ -175,3 +175,43 @@ def test_flowstream_lookahead_ring(lookahead):
             assert "k_wz_solve_c_next" in fs.plan.kernels()
     finally:
         fs.close()
+
+
+@pytest.mark.parametrize("producer_aligned", [True, False])
+def test_pipelined_dt0_across_gradient_flows(producer_aligned, monkeypatch):
+    """The fused gradient kernel (K12) is chosen per call by the frames' alignment (16-byte
+    planes): the dt0 a pipelined call formed lives where ITS flow puts it (Y4 with K12, Y0
+    without), so a consumer on the other flow must not take it (of3d_host.hip: pipe_k12) —
+    a producer whose window is 16-byte aligned and whose next window sits 8 bytes off (K12 ->
+    K1c + K2c), and the reverse: both calls bit-identical to the host entry point."""
+    import torch
+
+    monkeypatch.setenv("OF3D_K12", "1")  # K12 wherever the alignment allows, at this size
+    s, t, w = 2, 2, 5
+    rt = radii(s, t, w)[2]
+    nwin = 2 * rt + 1
+    shape = (24, 40, 48)
+    n = int(np.prod(shape))
+    stack = np.random.default_rng(77).integers(0, 4096, size=(nwin + 1,) + shape).astype(np.uint16)
+
+    def frames(k, aligned):
+        out = []
+        for i in range(nwin):
+            buf = torch.empty(n + 8, dtype=torch.int16, device="cuda")
+            v = buf[:n] if aligned else buf[4:4 + n]  # 8 bytes off: 8-byte but not 16-byte aligned
+            v.copy_(torch.from_numpy(stack[k + i].reshape(-1).view(np.int16)))
+            out.append(v)
+        return out
+
+    w0, w1 = frames(0, producer_aligned), frames(1, not producer_aligned)
+    assert (w0[rt].data_ptr() % 16 == 0) == producer_aligned and (w1[rt].data_ptr() % 16 == 0) != producer_aligned
+    plan = _lib.Plan(3, *shape, make_taps(s, t, w), device=0)
+    try:
+        got = _run(plan, [w0, w1], None, (0, shape[0]), shape, torch.float64, [(0, 1, True), (1, None, True)])
+        ks = plan.kernels()
+        assert "k_wz_solve_c_next" in ks and "k_grad_xyz_c" in ks and "k_grad_xy_c" in ks, ks
+    finally:
+        plan.close()
+    for k in range(2):
+        for a, b in zip(got[k], calc_flow3D(stack[k:k + nwin], s, t, w)):
+            assert bits_equal(a, b), (producer_aligned, k)

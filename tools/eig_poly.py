@@ -25,10 +25,11 @@ def horner(m, t):
     return v
 
 
-def deflate(aq, bq, cq, d, e, f, p, w):
+def deflate(aq, bq, cq, d, e, f, w):
     """csrc/of3d_dev.hpp eigmin3_deflate: the smaller eigenvalue of the near-degenerate pair of
-    E = T - qI from the 2x2 block on the plane orthogonal to lambda_max's eigenvector."""
-    mu = 2 * p * (1 - (2 / 9) * w)
+    B = (T - qI) / p from the 2x2 block on the plane orthogonal to lambda_max's eigenvector
+    (scaled: entries O(1) whatever the tensor's magnitude; the caller multiplies by p)."""
+    mu = 2 * (1 - (2 / 9) * w)
     m00, m11, m22 = aq - mu, bq - mu, cq - mu
     cr = [np.stack([d * f - e * m11, e * d - m00 * f, m00 * m11 - d * d], -1),
           np.stack([d * m22 - e * f, e * e - m00 * m22, m00 * f - d * e], -1),
@@ -78,17 +79,20 @@ def eigmin3(a, b, c, d, e, f, m=None, refine=False):
             sel = (w < DEFLATE_W) & (p1 != 0)
             if sel.any():
                 lam = lam.copy()
-                lam[sel] = q[sel] + deflate(aq[sel], bq[sel], cq[sel], d[sel], e[sel], f[sel], p[sel], w[sel])
+                lam[sel] = q[sel] + p[sel] * deflate(B11[sel], B22[sel], B33[sel], B12[sel], B13[sel], B23[sel],
+                                                     w[sel])
     return np.where(p1 == 0, np.minimum(a, np.minimum(b, c)), lam)
 
 
-def test_set(n=400000, seed=1, psd=False):
+def test_set(n=400000, seed=1, psd=False, extreme=False):
     """Symmetric 3x3 tensors with random orientation: generic spectra (three scales), and
     five hard sets — near-degenerate pairs, exact pairs (before rounding), a near-degenerate
-    smallest pair, near-isotropic, rank 1.  Returns (the six entries, eigvalsh)."""
+    smallest pair, near-isotropic, rank 1.  extreme: magnitudes 1e-100 / 1e100 too (fp64 only:
+    float32 cannot hold them).  Returns (the six entries, eigvalsh)."""
     rng = np.random.default_rng(seed)
     Q, _ = np.linalg.qr(rng.standard_normal((n, 3, 3)))
-    lam = rng.standard_normal((n, 3)) * rng.choice([1e-3, 1, 1e6], size=(n, 1))
+    scales = [1e-3, 1, 1e6] + ([1e-100, 1e100] if extreme else [])
+    lam = rng.standard_normal((n, 3)) * rng.choice(scales, size=(n, 1))
     if psd:
         lam = np.abs(lam)
     k = n // 6
