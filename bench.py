@@ -48,6 +48,10 @@ sys.path.insert(0, REPO)
 
 CONFIGS = {
     # name: (Nt, Nz, Ny, Nx, xyzSig, tSig, wSig, description)
+    # configs[0]: the reference's 2D example (calc_flow2D, calc_flow.py:18-173) as a series of 16
+    # frames (10 output frames); Nz = 1 marks the 2D path
+    "c1": (16, 1, 256, 256, 1, 1, 5, "configs[0]: 2D 256x256 x16 frames (SequenceT series, 10 output frames), "
+                                     "xySig=1 tSig=1 wSig=5, fp64 calc_flow2D on the GPU"),
     "c2": (13, 64, 256, 256, 2, 2, 5, "configs[1]: 3D OneTif 256x256x64 x13 frames (tSig=2), xyzSig=2 wSig=5, fp64"),
     "c3": (19, 128, 512, 512, 2, 3, 7, "configs[2]: 3D 512x512x128 x19 frames (tSig=3), xyzSig=2 wSig=7, fp64"),
     # configs[3]: one frame z-sharded over the ranks (strong scaling), halo exchange over RCCL
@@ -118,6 +122,106 @@ def synthetic_slab(nt, nz, ny, nx, z0, z1, seed, device, out=None, zchunk=32, ro
             noise = ((idx ^ (idx >> 7)) * 747796405 + 2891336453) % 17 - 8
             out[t, c0 - z0:c1 - z0] = torch.clamp(1000 + 300 * sv + noise, 0, 32767).to(torch.int16)
     return out
+
+
+def stage_model_2d(nt_win, rd, rs, rt, rw, plane):
+    """2D (calc_flow2D, calc_flow.py:18-173) per-launch algorithmic bytes / ops of each stage:
+    grad_xy = K0 + the y and x passes (dt: y(G) x(G); dy: y(D) x(S); dx: y(S) x(D)), products +
+    W y + W x of the five products, the 2x2 solve + rel (~30 ops: det, two products, the
+    discriminant's sqrt, two roots)."""
+    C = lambda r: 1 + 3 * r
+    return {
+        "grad_xy": {"bytes": (nt_win * 2 + 3 * 8) * plane, "ops": (C(rt) + 4 * C(rd) + 2 * C(rs)) * plane},
+        "grad_z": {"bytes": 0, "ops": 0},
+        "prod_wy_wx": {"bytes": (3 * 8 + 5 * 8) * plane, "ops": (5 + 10 * C(rw)) * plane},
+        "wz_solve": {"bytes": (5 * 8 + 3 * 8) * plane, "ops": 30 * plane},
+    }
+
+
+def run_2d(args, world, rank, dev):
+    """configs[0]: the 2D path (calc_flow2D) over a resident series of 16 frames (256 x 256,
+    xySig 1, tSig 1, wSig 5: 7-frame windows, 10 output frames).  One step = one output frame
+    (step i computes window i mod 10), the plan's four launches (K0, the y / x gradient passes,
+    K34 over the five products, the 2x2 solve).  N > 1: every rank its own series (replicas,
+    weak scaling).  cpu_baseline: the oracle's calc_flow2D over the same 10 windows, 1 thread."""
+    import torch
+    import torch.distributed as dist
+
+    from opticalflow3d_dev_amd import _lib, make_taps, radii
+
+    nt, _, ny, nx, s, t, w, desc = CONFIGS["c1"]
+    rd, rs, rt, rw = radii(s, t, w)
+    nwin = 2 * rt + 1
+    nout = nt - nwin + 1
+    d_in = synthetic_slab(nt, 1, ny, nx, 0, 1, 20260206 + 1 + 100 * rank, dev).view(nt, ny, nx)
+    plane = ny * nx
+    d_vx = torch.empty(plane, dtype=torch.float64, device=dev)
+    d_vy = torch.empty_like(d_vx)
+    d_rel = torch.empty_like(d_vx)
+    plan = _lib.Plan(2, 1, ny, nx, make_taps(s, t, w), device=dev.index, timing=max(args.steps, 1))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ptrs = [d_in[i].data_ptr() for i in range(nt)]
+    last = {"i": 0, "j": 0}
+
+    def step():
+        j = last["i"] % nout
+        last["i"] += 1
+        last["j"] = j
+        plan.execute(ptrs[j:j + nwin], _lib.OF3D_U16, 0, 0, 1, d_vx.data_ptr(), d_vy.data_ptr(), 0, d_rel.data_ptr(),
+                     stream)
+
+    elapsed, profile, dom, dom_ms = timed_region(step, plan, args, world, dev)
+    if world > 1:
+        (elapsed,) = max_over_ranks([elapsed], dev)
+    kernels = set(plan.kernels())
+    plan.close()
+    if rank != 0:
+        return
+    from oracle import cpu_ref
+
+    host = d_in.cpu().numpy().view(np.uint16)
+    j = last["j"]
+    want = cpu_ref.calc_flow2D(host[j:j + nwin], s, t, w, backend="scipy")
+    got = [d_vx.view(ny, nx).cpu().numpy(), d_vy.view(ny, nx).cpu().numpy(), d_rel.view(ny, nx).cpu().numpy()]
+    same = [np.array_equal(a.view(np.uint64), np.ascontiguousarray(b).view(np.uint64)) for a, b in zip(got, want)]
+    parity = {"ok": all(same), "crop_out": "whole frame (window %d)" % j,
+              "vx_vy_rel": "bitwise" if all(same) else "MISMATCH", "checker": "oracle/cpu_ref.py (scipy backend)"}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        from threadpoolctl import threadpool_limits
+
+        with threadpool_limits(limits=1):
+            reps, t0 = 0, time.perf_counter()
+            while True:  # whole passes over the series' 10 output frames, ~min(budget, 10 s)
+                for k in range(nout):
+                    cpu_ref.calc_flow2D(host[k:k + nwin], s, t, w, backend="scipy")
+                reps += 1
+                dt = time.perf_counter() - t0
+                if dt >= min(args.cpu_budget, 10.0):
+                    break
+        cpu = {"value": round(reps * nout * plane / dt / 1e6, 4), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} passes over the series' {nout} output frames ({ny}x{nx}, {nwin}-frame windows): "
+                         f"oracle/cpu_ref.py calc_flow2D (scipy.ndimage.correlate1d), 1 thread, {dt:.2f} s",
+               "seconds": round(dt, 3), "host_cpus": os.cpu_count(),
+               **calibrated(reps * nout * plane / dt / 1e6, "c1")}
+    C = lambda r: 1 + 3 * r
+    frame_ops = (C(rt) + 4 * C(rd) + 2 * C(rs) + 5 + 10 * C(rw) + 30) * plane
+    roof = roofline(profile, dom, dom_ms, stage_model_2d(nwin, rd, rs, rt, rw, plane), "c1",
+                    (nwin * 2 + 3 * 8) * plane, frame_ops, nwin, 8, used=kernels)
+    roof["frame"]["bytes_per_voxel"] = nwin * 2 + 3 * 8  # vx, vy, rel: fp64 (2D rel is fp64)
+    ms = elapsed / args.steps * 1e3
+    line = {
+        "metric": "Mvoxels/s per frame-pair (and HBM GB/s fraction) at 1/2/4/8 MI355X",
+        "value": round(world * plane * args.steps / elapsed / 1e6, 3), "unit": "Mvoxels/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": desc, "nt": nt, "nt_window": nwin, "ny": ny, "nx": nx, "xySig": s, "tSig": t, "wSig": w,
+                   "parallelism": f"series replicas x{world}" if world > 1 else "single GPU",
+                   "inputs": f"a series of {nt} uint16 frames resident in HBM; step i computes output frame i mod {nout}",
+                   "kernels": sorted(kernels)},
+        "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "build": build_stamp(),
+    }
+    print(json.dumps(line), flush=True)
 
 
 def stage_model(nt_win, rd, rs, rt, rw, nb, ng, no, plane, sv=8):
@@ -964,7 +1068,7 @@ def main():
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="default: c3 = configs[2] on one GPU (the single-GPU headline); at N > 1 the volume "
                          "the BASELINE config names for N GPUs, z-sharded over the ranks: c4 = configs[3] "
-                         "(2 and 4 GPUs), c5 = configs[4] (8 GPUs); c2 = configs[1]")
+                         "(2 and 4 GPUs), c5 = configs[4] (8 GPUs); c2 = configs[1]; c1 = configs[0] (2D)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--overlap", type=int, default=int(os.environ.get("OF3D_BENCH_OVERLAP", "-1")),
                     help="z chunk (output planes) of the plan's overlap mode; 0 = serial; -1 = the plan's default")
@@ -1014,6 +1118,11 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    if args.config == "c1":
+        run_2d(args, world, rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.config in ZSLAB_CONFIGS or (world > 1 and not explicit):
         run_slab(args, world, rank, local_rank, dev)
         if world > 1:

@@ -14,7 +14,8 @@
  *  - Host entry points (of3d_flow3d / of3d_flow2d): the caller owns every host
  *    buffer; the library owns device memory (cached per shape+taps).
  *  - Device entry point (of3d_plan_execute): every pointer is device memory,
- *    work is enqueued on the given HIP stream (NULL = the plan's stream) and
+ *    work is enqueued on the given HIP stream (NULL = the device's null stream,
+ *    HIP's own convention: ordered with the caller's default-stream work) and
  *    the call returns without synchronising.
  *  - Return 0 on success; non-zero = error, text in of3d_last_error()
  *    (thread-local).  The Python host maps the reference's argument checks
@@ -145,7 +146,9 @@ int of3d_plan_input_range(const of3d_plan* plan, int64_t z_out0, int64_t z_out1,
  * d_vx/d_vy/d_vz: float64 (z_out1-z_out0, ny, nx) (d_vz ignored for 2D);
  * d_rel: float32 for 3D (float64 if the plan's mode has OF3D_REL_F64),
  * float64 for 2D.  OF3D_FP32 plans: every output float32.
- * stream: hipStream_t or NULL. */
+ * stream: hipStream_t, or NULL for the null stream (round 5; it used to mean the plan's own
+ * non-blocking stream, which a torch caller passing its default stream's handle 0 got
+ * unordered with its own kernels). */
 int of3d_plan_execute(of3d_plan* plan, const void* const* d_frames, int dtype, int64_t frame_z0,
                       int64_t z_out0, int64_t z_out1, void* d_vx, void* d_vy, void* d_vz,
                       void* d_rel, void* stream);

@@ -44,14 +44,16 @@ const void* k34_fn_uq(int rw, int s) {
     return nullptr;
 }
 
-// Wave-specialised instances (k_prod_wyx_ws: 8 producer + 8 consumer waves, 512 staged
-// columns, 128 VGPRs)
+// Wave-specialised instances (k_prod_wyx_ws: npw producer + 16 - npw consumer waves, 64 npw
+// staged columns, 128 VGPRs): npw 8 (512 staged columns), and in fp64 npw 9 (576: two blocks
+// per 1024-wide row)
 template <typename F, int NP>
-const void* k34_fn_ws(int rw, int s) {
-#define OF3D_K34W(RW)                                                              \
-    if (rw == RW) {                                                                \
-        if (s == 8) return (const void*)k_prod_wyx_ws<F, NP, RW, 8>;               \
-        if (s == 4) return (const void*)k_prod_wyx_ws<F, NP, RW, 4>;               \
+const void* k34_fn_ws(int rw, int s, int npw) {
+    if (npw != 8 && (npw != 9 || sizeof(F) != 8)) return nullptr;
+#define OF3D_K34W(RW)                                                                                              \
+    if (rw == RW) {                                                                                                \
+        if (s == 8) return npw == 8 ? (const void*)k_prod_wyx_ws<F, NP, RW, 8> : (const void*)k_prod_wyx_ws<F, NP, RW, 8, 2, 2, 9>; \
+        if (s == 4) return npw == 8 ? (const void*)k_prod_wyx_ws<F, NP, RW, 4> : (const void*)k_prod_wyx_ws<F, NP, RW, 4, 2, 2, 9>; \
     }
     OF3D_K34W(21)
     OF3D_K34W(18)
@@ -81,10 +83,10 @@ const void* k34_fn_pk(int rw, int s) {
 template const void* k34_fn_pk<9>(int, int);
 template const void* k34_fn_pk<5>(int, int);
 
-template const void* k34_fn_ws<double, 9>(int, int);
-template const void* k34_fn_ws<double, 5>(int, int);
-template const void* k34_fn_ws<float, 9>(int, int);
-template const void* k34_fn_ws<float, 5>(int, int);
+template const void* k34_fn_ws<double, 9>(int, int, int);
+template const void* k34_fn_ws<double, 5>(int, int, int);
+template const void* k34_fn_ws<float, 9>(int, int, int);
+template const void* k34_fn_ws<float, 5>(int, int, int);
 template const void* k34_fn_uq<double, 9>(int, int);
 template const void* k34_fn_uq<double, 5>(int, int);
 template const void* k34_fn_uq<float, 9>(int, int);

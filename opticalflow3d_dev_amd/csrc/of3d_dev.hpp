@@ -1014,11 +1014,15 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 // scheduler issued half of its ops right behind the op they depend on; with them 2 %.  Same ops,
 // same order per chain (bit-identical).  c3 K34 1.665 -> 1.631 ms, c4 equal
 // (profiles/r04/ab_k34ilp/).  The packed fp32 kernel spills with it and keeps its form.
-template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2>
+// NPW: producer waves (staged columns 64 NPW), the other 16 - NPW consume.  8 + 8 suits a row
+// whose blocks stage 512 columns (c3: the whole 512-wide row, no halo); 9 + 7 lets a 1024-wide
+// row (c4) take two blocks of 512 outputs + 15 halo columns (527 staged) instead of three of 344
+// (374 staged: two of the eight producer waves idle, a third of the consumers' capacity unused).
+template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2, int NPW = 8>
 __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
                                                       size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
                                                       int nyb, int cpg, int ngroups, int yb0, int yb1) {
-    constexpr int RB = 4, CWA = 512;
+    constexpr int RB = 4, CWA = 64 * NPW, NCT = 1024 - CWA;  // producer threads; consumer threads
     constexpr int NR = k34_nr(RW, S);
     constexpr unsigned ES = sizeof(F);
     static_assert(NR % PD == 0 && NR % S == 0, "ring sizes");
@@ -1154,7 +1158,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
             lds_barrier();  // tile tt written
             const F* tile = sw + (tt & 1) * k34_tile(S, cwp);
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
-            for (int i = tb; i < 64 * RG * nsgw; i += CWA) {
+            for (int i = tb; i < 64 * RG * nsgw; i += NCT) {
                 const int l = i & 63, wg = i >> 6;
                 const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
                 const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));

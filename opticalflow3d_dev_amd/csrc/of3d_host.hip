@@ -304,7 +304,34 @@ int k34_setup(of3d_plan* p, int np) {
         waves = nb * (cw / 64);
         return 0;
     };
+    // the unique-staging column stride for blocks of cw staged columns: fewest staged lanes (64 per
+    // started wave of each block), ties to the wider stride (fewer blocks); 0: none fits
+    auto uq_stride = [&](int cw) {
+        int tx = 0;
+        long lanes = 0;
+        for (int nbx = 1; nbx <= 64; ++nbx) {
+            const int t = nbx == 1 ? nx : ((nx + nbx - 1) / nbx + 3) & ~3;
+            if (t < 8) break;
+            int widest = 0;
+            const long l = k34_lanes(nx, rw, t, widest);
+            if (widest > cw) continue;
+            if (!tx || l < lanes) tx = t, lanes = l;
+        }
+        return tx;
+    };
     for (int s : {16, 8, 4}) {
+        // wave-specialised with 9 producer waves (576 staged columns, fp64): rows whose 512-column
+        // blocks would need more than 512 staged columns (nx 1024: 2 x (512 + 15) instead of 3 x 344)
+        if (const void* f9 = (uq != 0 && uq != 1 && uq != 3 && kn.k34_ws)
+                                 ? (np == 9 ? k34_fn_ws<F, 9>(rw, s, 9) : k34_fn_ws<F, 5>(rw, s, 9)) : nullptr) {
+            const int tx = uq_stride(576), tx8 = uq_stride(512);
+            if (tx && (!tx8 || (nx + tx - 1) / tx < (nx + tx8 - 1) / tx8)) {  // only where it saves blocks
+                const size_t lds = (size_t)2 * k34_tile(s, k34_pitch(std::min(tx, nx), rw)) * es;
+                int w9 = 0;
+                if (lds <= 160 * 1024 && !occupancy(f9, 1024, lds, w9) && w9 >= 16)
+                    p->k34_cand.push_back({f9, 576, s, tx, (nx + tx - 1) / tx, lds, 1024});
+            }
+        }
         const void* fd = uq == 1 ? nullptr : (np == 9 ? k34_fn<F, 9>(rw, s, 4) : k34_fn<F, 5>(rw, s, 4));
         const void* fu = uq == 0 ? nullptr : (np == 9 ? k34_fn_uq<F, 9>(rw, s) : k34_fn_uq<F, 5>(rw, s));
         for (int nw : {1, 2, 3, 4, 8}) {  // launch bound 512
@@ -332,16 +359,7 @@ int k34_setup(of3d_plan* p, int np) {
                 }
             }
             if (fu && nw >= 4) {  // unique staging: the column stride with the fewest staged lanes
-                int tx = 0;
-                long lanes = 0;
-                for (int nbx = 1; nbx <= 64; ++nbx) {
-                    const int t = nbx == 1 ? nx : ((nx + nbx - 1) / nbx + 3) & ~3;
-                    if (t < 8) break;
-                    int widest = 0;
-                    const long l = k34_lanes(nx, rw, t, widest);
-                    if (widest > cw) continue;
-                    if (!tx || l < lanes) tx = t, lanes = l;  // ties: the wider stride, fewer blocks
-                }
+                const int tx = uq_stride(cw);
                 if (tx) {
                     const int nbx = (nx + tx - 1) / tx;
                     const size_t lds = (size_t)2 * k34_tile(s, k34_pitch(std::min(tx, nx), rw)) * es;
@@ -350,7 +368,7 @@ int k34_setup(of3d_plan* p, int np) {
                         p->k34_cand.push_back({fu, cw, s, tx, nbx, lds});
                     // the wave-specialised form of the same geometry (8 producer + 8 consumer waves)
                     const void* fw =
-                (nw == 8 && kn.k34_ws) ? (np == 9 ? k34_fn_ws<F, 9>(rw, s) : k34_fn_ws<F, 5>(rw, s)) : nullptr;
+                (nw == 8 && kn.k34_ws) ? (np == 9 ? k34_fn_ws<F, 9>(rw, s, 8) : k34_fn_ws<F, 5>(rw, s, 8)) : nullptr;
                     int wsw = 0;
                     if (fw && lds <= 160 * 1024 && !occupancy(fw, 2 * cw, lds, wsw) && wsw >= 2 * nw)
                         p->k34_cand.push_back({fw, cw, s, tx, nbx, lds, 2 * cw});
@@ -1258,6 +1276,7 @@ void plan_free(of3d_plan* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
+    (void)hipDeviceSynchronize();  // executions on callers' streams may still read the workspace
     (void)hipFree(p->d_taps);
     (void)hipFree(p->d_taps32);
     (void)hipFree(p->X);
@@ -1492,7 +1511,7 @@ int of3d_plan_execute(of3d_plan* p, const void* const* d_frames, int dtype, int6
                       void* vx, void* vy, void* vz, void* rel, void* stream) {
     if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
     OF3D_HIP(hipSetDevice(p->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the device's null stream (HIP's convention)
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s);
 }
 
@@ -1501,7 +1520,7 @@ int of3d_plan_execute_next(of3d_plan* p, const void* const* d_frames, const void
                            void* stream) {
     if (!p || !d_frames || !vx || !vy || !rel || (p->ndim == 3 && !vz)) return fail("of3d: null argument");
     OF3D_HIP(hipSetDevice(p->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the device's null stream (HIP's convention)
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_frames_next, true);
 }
 
@@ -1511,7 +1530,7 @@ int of3d_plan_execute_ahead(of3d_plan* p, const void* const* d_frames, int n_ahe
     if (n_ahead < 0) return fail("of3d: n_ahead out of range");
     n_ahead = std::min(n_ahead, kMaxT - (2 * p->rt + 1));  // frames past kMaxT are not batched
     OF3D_HIP(hipSetDevice(p->device));
-    hipStream_t s = stream ? (hipStream_t)stream : p->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL: the device's null stream (HIP's convention)
     return run(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, nullptr, false, n_ahead);
 }
 
@@ -1519,8 +1538,7 @@ int of3d_plan_set_timing(of3d_plan* p, int slots) {
     if (!p) return fail("of3d: null plan");
     if (slots < 0 || slots > 4096) return fail("of3d: timing slots must be in [0, 4096]");
     OF3D_HIP(hipSetDevice(p->device));
-    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
-    if (p->stream2) OF3D_HIP(hipStreamSynchronize(p->stream2));
+    OF3D_HIP(hipDeviceSynchronize());  // executions may sit on any caller stream: events idle first
     for (auto e : p->tev) (void)hipEventDestroy(e);
     p->tev_per_slot = std::max(kStages + 1, 2 * kMaxChunks);
     p->tev.assign((size_t)slots * p->tev_per_slot, nullptr);
@@ -1536,7 +1554,7 @@ int of3d_plan_set_timing_mask(of3d_plan* p, unsigned mask) {
     mask &= (1u << kStages) - 1;
     if (!mask) return fail("of3d: timing mask selects no stage");
     OF3D_HIP(hipSetDevice(p->device));
-    if (p->stream) OF3D_HIP(hipStreamSynchronize(p->stream));
+    OF3D_HIP(hipDeviceSynchronize());
     p->timing_mask = mask;
     p->tcount = 0;
     return 0;
