@@ -16,7 +16,7 @@ template <typename F> const void* k3_kernel(int np, int rw);                 // 
 template <typename F> const void* k4_kernel(int nf, int rw);                 // kt_prod_legacy.hip
 template <typename F, int NP> const void* k34_fn(int rw, int s, int rb);     // kt_prod.hip
 template <typename F, int NP> const void* k34_fn_uq(int rw, int s);         // kt_prod.hip (8-wave, unique staging)
-template <typename F, int NP> const void* k34_fn_ws(int rw, int s, int npw);  // kt_prod.hip (16-wave, specialised)
+template <typename F, int NP> const void* k34_fn_ws(int rw, int s, int npw, int pd);  // kt_prod.hip (16-wave, specialised)
 template <int NP> const void* k34_fn_pk(int rw, int s);                        // kt_prod.hip (packed fp32)
 template <typename F, typename RelT> const void* k5_kernel(int rw);          // kt_solve_legacy.hip
 template <typename F, typename RelT> const void* k5_dma_kernel(int rw, int nb);  // kt_solve_legacy.hip

@@ -47,9 +47,22 @@ const void* k34_fn_uq(int rw, int s) {
 // Wave-specialised instances (k_prod_wyx_ws: npw producer + 16 - npw consumer waves, 64 npw
 // staged columns, 128 VGPRs): npw 8 (512 staged columns), and in fp64 npw 9 (576: two blocks
 // per 1024-wide row)
+// pd: gradient prefetch rows of the producers (2; 4 for fp64 radii up to 15 at 4-row tiles,
+// where the 2 rw + 2 row register ring leaves the room)
 template <typename F, int NP>
-const void* k34_fn_ws(int rw, int s, int npw) {
+const void* k34_fn_ws(int rw, int s, int npw, int pd) {
     if (npw != 8 && (npw != 9 || sizeof(F) != 8)) return nullptr;
+    if (pd == 4) {
+        if (sizeof(F) != 8 || s != 4) return nullptr;
+#define OF3D_K34W4(RW) \
+        if (rw == RW) return npw == 8 ? (const void*)k_prod_wyx_ws<F, NP, RW, 4, 4, 2, 8> : (const void*)k_prod_wyx_ws<F, NP, RW, 4, 4, 2, 9>;
+        OF3D_K34W4(15)
+        OF3D_K34W4(12)
+        OF3D_K34W4(9)
+#undef OF3D_K34W4
+        return nullptr;
+    }
+    if (pd != 2) return nullptr;
 #define OF3D_K34W(RW)                                                                                              \
     if (rw == RW) {                                                                                                \
         if (s == 8) return npw == 8 ? (const void*)k_prod_wyx_ws<F, NP, RW, 8> : (const void*)k_prod_wyx_ws<F, NP, RW, 8, 2, 2, 9>; \
@@ -83,10 +96,10 @@ const void* k34_fn_pk(int rw, int s) {
 template const void* k34_fn_pk<9>(int, int);
 template const void* k34_fn_pk<5>(int, int);
 
-template const void* k34_fn_ws<double, 9>(int, int, int);
-template const void* k34_fn_ws<double, 5>(int, int, int);
-template const void* k34_fn_ws<float, 9>(int, int, int);
-template const void* k34_fn_ws<float, 5>(int, int, int);
+template const void* k34_fn_ws<double, 9>(int, int, int, int);
+template const void* k34_fn_ws<double, 5>(int, int, int, int);
+template const void* k34_fn_ws<float, 9>(int, int, int, int);
+template const void* k34_fn_ws<float, 5>(int, int, int, int);
 template const void* k34_fn_uq<double, 9>(int, int);
 template const void* k34_fn_uq<double, 5>(int, int);
 template const void* k34_fn_uq<float, 9>(int, int);
