@@ -2086,6 +2086,73 @@ __device__ __forceinline__ double eigmin3(double a, double b, double c, double d
     return q - 2.0 * p * cos_two_thirds_acos(w * iu);
 }
 
+// eigmin3 for G tensors at once, straight-line: the per-tensor branches of eigmin3 become
+// per-lane selects, and its rare paths (tensors too small / large for the rsq estimate; the
+// fp64-rel deflation) wave-uniform branches taken only when some lane of the wave needs them.
+// Every tensor goes through exactly eigmin3<REFINE>'s operations (bit-identical), but as G
+// independent chains the scheduler can interleave: K5c's epilogue ran one dependent chain per
+// voxel (IEEE divisions, rsq Newton steps, the polynomial) with two waves per SIMD to hide it.
+template <bool REFINE, int G>
+__device__ __forceinline__ void eigmin3_group(const double (&a)[G], const double (&b)[G], const double (&c)[G],
+                                              const double (&d)[G], const double (&e)[G], const double (&f)[G],
+                                              double (&out)[G]) {
+    constexpr double third = 1.0 / 3.0, sixth = 1.0 / 6.0;
+    double q[G], aq[G], bq[G], cq[G], x[G], p[G], ip[G];
+    bool diag[G], slow[G], any_slow = false;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        const double p1 = d[i] * d[i] + e[i] * e[i] + f[i] * f[i];
+        diag[i] = p1 == 0.0;
+        q[i] = (a[i] + b[i] + c[i]) * third;
+        aq[i] = a[i] - q[i], bq[i] = b[i] - q[i], cq[i] = c[i] - q[i];
+        const double p2 = aq[i] * aq[i] + bq[i] * bq[i] + cq[i] * cq[i] + 2.0 * p1;
+        x[i] = p2 * sixth;
+        double r = __builtin_amdgcn_rsq(x[i]);
+        r = r * (1.5 - 0.5 * x[i] * r * r);
+        r = r * (1.5 - 0.5 * x[i] * r * r);
+        ip[i] = r;
+        p[i] = x[i] * r;
+        slow[i] = !diag[i] && !(x[i] > 1e-290 && x[i] < 1e290);
+        any_slow |= slow[i];
+    }
+    if (__builtin_expect(__any(any_slow), 0)) {  // IEEE sqrt / division where rsq cannot serve
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+            if (slow[i]) {
+                p[i] = sqrt(x[i]);
+                ip[i] = 1.0 / p[i];
+            }
+    }
+    double B11[G], B22[G], B33[G], B12[G], B13[G], B23[G], w[G];
+    bool defl[G], any_defl = false;
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+        B11[i] = aq[i] * ip[i], B22[i] = bq[i] * ip[i], B33[i] = cq[i] * ip[i];
+        B12[i] = d[i] * ip[i], B13[i] = e[i] * ip[i], B23[i] = f[i] * ip[i];
+        const double detB = B11[i] * (B22[i] * B33[i] - B23[i] * B23[i]) - B12[i] * (B12[i] * B33[i] - B23[i] * B13[i]) +
+                            B13[i] * (B12[i] * B23[i] - B22[i] * B13[i]);
+        double r = 0.5 * detB;
+        r = fmin(1.0, fmax(-1.0, r));
+        w[i] = fmax((1.0 - r) * 0.5, 1e-290);
+        defl[i] = REFINE && !diag[i] && w[i] < 1e-6;
+        any_defl |= defl[i];
+        double iu = __builtin_amdgcn_rsq(w[i]);
+        iu = iu * (1.5 - 0.5 * w[i] * iu * iu);
+        iu = iu * (1.5 - 0.5 * w[i] * iu * iu);
+        out[i] = q[i] - 2.0 * p[i] * cos_two_thirds_acos(w[i] * iu);
+    }
+    if constexpr (REFINE) {
+        if (__builtin_expect(__any(any_defl), 0)) {
+#pragma unroll
+            for (int i = 0; i < G; ++i)
+                if (defl[i]) out[i] = q[i] + p[i] * eigmin3_deflate(B11[i], B22[i], B33[i], B12[i], B13[i], B23[i], w[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+        if (diag[i]) out[i] = fmin(a[i], fmin(b[i], c[i]));
+}
+
 // K5: W z pass + solve + reliability.  Block = 64 x-columns of one row and
 // K5_ZC output planes; per field the (K5_ZC + 2rw)-plane clamped window is
 // staged in LDS (double-buffered, next field's loads in flight during this
@@ -2100,23 +2167,53 @@ constexpr K5Geom k5_geom(int rw) { return {rw <= 24 ? 8 : 4, 8}; }
 
 // Pointwise tail of K5: solve + reliability for the thread's R planes, in
 // fp64 whatever the pass type F (fp32 plans solve their float tensor in fp64).
-template <typename F, typename RelT, int K5_R>
+// (K5c: G voxels at a time through solve3 and eigmin3_group — straight-line code, G independent
+// chains; the legacy kernels keep G = 1, the same operations per voxel: bit-identical)
+template <typename F, typename RelT, int K5_R, int G = 1>
 __device__ __forceinline__ void k5_solve_store(const F (&acc)[9][K5_R], int z0l, int nzo, size_t o0, size_t ps,
                                                F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz,
                                                RelT* __restrict__ rel) {
+    static_assert(K5_R % G == 0, "voxel groups");
+    if constexpr (G == 1) {
 #pragma unroll
-    for (int i = 0; i < K5_R; ++i) {
-        if (z0l + i >= nzo) break;
-        // field order: tx ty tz xy xz x2 yz y2 z2
-        const double tx = acc[0][i], ty = acc[1][i], tz = acc[2][i], xy = acc[3][i], xz = acc[4][i],
-                     x2 = acc[5][i], yz = acc[6][i], y2 = acc[7][i], z2 = acc[8][i];
-        double ox, oy, oz;
-        solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
-        const size_t o = (size_t)(z0l + i) * ps + o0;
-        vx[o] = (F)ox;
-        vy[o] = (F)oy;
-        vz[o] = (F)oz;
-        rel[o] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
+        for (int i = 0; i < K5_R; ++i) {
+            if (z0l + i >= nzo) break;
+            // field order: tx ty tz xy xz x2 yz y2 z2
+            const double tx = acc[0][i], ty = acc[1][i], tz = acc[2][i], xy = acc[3][i], xz = acc[4][i],
+                         x2 = acc[5][i], yz = acc[6][i], y2 = acc[7][i], z2 = acc[8][i];
+            double ox, oy, oz;
+            solve3(x2, y2, z2, xy, xz, yz, tx, ty, tz, ox, oy, oz);
+            const size_t o = (size_t)(z0l + i) * ps + o0;
+            vx[o] = (F)ox;
+            vy[o] = (F)oy;
+            vz[o] = (F)oz;
+            rel[o] = (RelT)eigmin3<std::is_same_v<RelT, double>>(x2, y2, z2, xy, xz, yz);
+        }
+    } else {
+#pragma unroll
+        for (int g0 = 0; g0 < K5_R; g0 += G) {
+            if (z0l + g0 >= nzo) break;
+            double x2[G], y2[G], z2[G], xy[G], xz[G], yz[G], lam[G];
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const int k = g0 + i;
+                const double tx = acc[0][k], ty = acc[1][k], tz = acc[2][k];
+                xy[i] = acc[3][k], xz[i] = acc[4][k], x2[i] = acc[5][k], yz[i] = acc[6][k], y2[i] = acc[7][k],
+                z2[i] = acc[8][k];
+                double ox, oy, oz;
+                solve3(x2[i], y2[i], z2[i], xy[i], xz[i], yz[i], tx, ty, tz, ox, oy, oz);
+                if (z0l + k < nzo) {
+                    const size_t o = (size_t)(z0l + k) * ps + o0;
+                    vx[o] = (F)ox;
+                    vy[o] = (F)oy;
+                    vz[o] = (F)oz;
+                }
+            }
+            eigmin3_group<std::is_same_v<RelT, double>, G>(x2, y2, z2, xy, xz, yz, lam);
+#pragma unroll
+            for (int i = 0; i < G; ++i)
+                if (z0l + g0 + i < nzo) rel[(size_t)(z0l + g0 + i) * ps + o0] = (RelT)lam[i];
+        }
     }
 }
 
@@ -2225,6 +2322,8 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
     if (x >= nx) return;
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
+
+constexpr int K5C_G = 4;  // voxels per straight-line group in K5c's epilogue (k5_solve_store)
 
 // K5c block coordinates from the launch's (columns, rows, z chunks) grid, XCD-aware: the
 // linear workgroup id b runs on XCD b % 8, so the z chunks of one (column block, row) — whose
@@ -2340,7 +2439,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
     if (x < nx)
-        k5_solve_store<F, RelT, R>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
+        k5_solve_store<F, RelT, R, K5C_G>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
                                    vy, vz, rel);
     if constexpr (RT0 > 0) {  // the next frame's dt0: the held groups, then any rest of [k0g0, k0g1)
 #pragma unroll
