@@ -815,6 +815,27 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
     }
 }
 
+// W-xy hand-off layout (K34 writes, K5c reads; csrc/of3d_host.hip picks it per plan).
+// zt == 0: field-major planes [z][y][x].  zt > 0 (zt = the workspace's planes): z-tiled
+// [y][x / 32][z][32] — K5c's block (32 columns of one row, ZC + 2 RW planes) then reads each field
+// window as ONE contiguous run instead of ZC + 2 RW pieces of 256 B a plane apart: the window
+// reads alone take 0.385 instead of 0.488 ms at c3, 3.13 instead of 4.0-4.2 ms at c4
+// (tools/mb_window.hip).  K34 stores per tile of rows from yb: a buffer descriptor at the tile's
+// first element and 32-bit per-lane byte offsets (a tile of S rows spans S nx zt elements).
+template <typename F>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wxy_rsrc(F* Qp, int zl, int yb, int xo0, int ny, int nx, int zt) {
+    return zt ? buf_rsrc(Qp + ((size_t)yb * nx * zt + (size_t)zl * 32)) : buf_rsrc(Qp + ((size_t)zl * ny + yb) * nx + xo0);
+}
+// byte offset of row r (of the tile) at column x = xo0 + c0 (c0 + RB - 1 in the same 32-column
+// tile: RB | 32 and xo0 a multiple of RB)
+template <typename F>
+__device__ __forceinline__ unsigned wxy_off(int r, int xo0, int c0, int nx, int zt) {
+    const int x = xo0 + c0;
+    return zt ? ((unsigned)r * (unsigned)nx * (unsigned)zt + (unsigned)(x >> 5) * (unsigned)zt * 32u + (unsigned)(x & 31)) *
+                    (unsigned)sizeof(F)
+              : ((unsigned)r * (unsigned)nx + (unsigned)c0) * (unsigned)sizeof(F);
+}
+
 // OCC: waves per SIMD the register budget is cut for (3: 168 VGPRs; 2: 256, for 8-wave blocks,
 // which run one per CU anyway); PDX: gradient prefetch rows (0: as far as OCC 3 allows);
 // DB: LDS prefetch distance of the phase-B pass; UQ: staging (below).
@@ -823,7 +844,7 @@ template <typename F, int NP, int RW, int S, int RB = 4, int OCC = 3, int PDX = 
 __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, F* __restrict__ Q, int ny,
                                                        int nx, size_t fs, const F* __restrict__ hw, int tx,
                                                        int nyc, int nbx, int nyb, int cpg, int ngroups, int yb0,
-                                                       int yb1) {
+                                                       int yb1, int zt) {
     constexpr int NR = k34_nr(RW, S);
     // gradient prefetch distance (rows): as far as 168 VGPRs (3 waves/SIMD) allow
     constexpr int PD0 = PDX ? PDX : (sizeof(F) == 8 ? (RW >= 18 ? 2 : 4) : (RW >= 18 ? 4 : 8));
@@ -892,7 +913,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const size_t pl = (size_t)zl * ny * nx;
     const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
     const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
-    const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+    F* const Qp = Q + (size_t)p * fs;
     const unsigned rowb = (unsigned)nx * ES;
     F h[RW + 1];
 #pragma unroll
@@ -925,6 +946,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const int nsgw = (nseg + SPW - 1) / SPW;
     auto phase_b = [&](const F* tile, int yb, int nr) {
         lds_barrier();
+        const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
         for (int i = t; i < 64 * RG * nsgw; i += ca) {
             const int l = i & 63, wg = i >> 6;
             const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
@@ -935,7 +957,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
             if (r < nr) {
                 // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
                 const int c0 = RB * sg;
-                const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
+                const unsigned vo = wxy_off<F>(r, xo0, c0, nx, zt);
                 if (c0 + RB <= txu) {
                     buf_st_n<F, RB>(out, rq_, vo, 0);
                 } else {
@@ -1021,7 +1043,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
 template <typename F, int NP, int RW, int S, int PD = 2, int DB = 2, int NPW = 8>
 __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F* __restrict__ Q, int ny, int nx,
                                                       size_t fs, const F* __restrict__ hw, int tx, int nyc, int nbx,
-                                                      int nyb, int cpg, int ngroups, int yb0, int yb1) {
+                                                      int nyb, int cpg, int ngroups, int yb0, int yb1, int zt) {
     constexpr int RB = 4, CWA = 64 * NPW, NCT = 1024 - CWA;  // producer threads; consumer threads
     constexpr int NR = k34_nr(RW, S);
     constexpr unsigned ES = sizeof(F);
@@ -1149,7 +1171,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
         }
     } else {
         const int tb = t - CWA;
-        const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+        F* const Qp = Q + (size_t)p * fs;
         const int nseg = (txu + RB - 1) / RB;
         constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW;
         constexpr int RG = S / RPW;
@@ -1158,6 +1180,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
             lds_barrier();  // tile tt written
             const F* tile = sw + (tt & 1) * k34_tile(S, cwp);
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
+            const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
             for (int i = tb; i < 64 * RG * nsgw; i += NCT) {
                 const int l = i & 63, wg = i >> 6;
                 const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
@@ -1167,7 +1190,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                 lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
                 if (r < nr) {
                     const int c0 = RB * sg;
-                    const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * ES;
+                    const unsigned vo = wxy_off<F>(r, xo0, c0, nx, zt);
                     if (c0 + RB <= txu) {
                         buf_st_n<F, RB>(out, rq_, vo, 0);
                     } else {
@@ -1194,7 +1217,7 @@ template <int NP, int RW, int S, int PD = 2, int DB = 2>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_prod_wyx_pk(const float* __restrict__ G, float* __restrict__ Q, int ny,
                                                      int nx, size_t fs, const float* __restrict__ hw, int tx,
                                                      int nyc, int nbx, int nyb, int cpg, int ngroups, int yb0,
-                                                     int yb1) {
+                                                     int yb1, int zt) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     constexpr int RB = 4, NPT = 256;  // outputs per consumer item; producer (= consumer) threads
     constexpr int NR = k34_nr(RW, S);
@@ -1331,7 +1354,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
     } else {
         const int tb = t - NPT;
-        const auto rq_ = buf_rsrc(Q + (size_t)p * fs + pl + xo0);
+        float* const Qp = Q + (size_t)p * fs;
         const int nseg = (txu + RB - 1) / RB;
         constexpr int PP = S / 2, SPW = 64 / PP;  // pairs per tile; segments per wave item
         const int nsgw = (nseg + SPW - 1) / SPW;
@@ -1339,6 +1362,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             lds_barrier();  // tile tt written
             const f2* tile = sw + (tt & 1) * TB;
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
+            const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
             for (int i = tb; i < 64 * nsgw; i += NPT) {
                 const int l = i & 63, wg = i >> 6;
                 const int pr = l % PP, sg = wg * SPW + l / PP;
@@ -1353,7 +1377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                         float o[RB];
 #pragma unroll
                         for (int e = 0; e < RB; ++e) o[e] = e2 ? out[e].y : out[e].x;
-                        const unsigned vo = (unsigned)(yb + r) * rowb + (unsigned)c0 * 4u;
+                        const unsigned vo = wxy_off<float>(r, xo0, c0, nx, zt);
                         if (c0 + RB <= txu) {
                             buf_st_n<float, RB>(o, rq_, vo, 0);
                         } else {
@@ -2362,7 +2386,7 @@ __device__ __forceinline__ K5Block k5c_block() {
 template <typename F, typename RelT, int RW, int NB, int R, int NW = 4, int RT0 = 0, typename T0 = uint16_t>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_solve_c(
     const F* __restrict__ Q, int zq0, int nz, int ny, int nx, size_t fs, const F* __restrict__ hw, int zo0, int nzo,
-    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel, int yo0, K0Next<F> k0) {
+    F* __restrict__ vx, F* __restrict__ vy, F* __restrict__ vz, RelT* __restrict__ rel, int yo0, K0Next<F> k0, int zt) {
     // NW 8: 128-plane blocks (one per CU), window 1.33x the output planes instead of 1.66x
     constexpr int CB = 32, LPC = 64 / CB;  // columns per block, z-groups per wave
     constexpr int ZC = NW * LPC * R;                // output planes per block (R planes per z-group)
@@ -2382,7 +2406,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
     const int zc0 = zo0 + kb.bz * ZC;
     const size_t ps = (size_t)ny * nx;
     const int xc = min(kb.bx * CB + EPL * (lane % LPR), nx - EPL);  // this lane's DMA columns
-    const F* qrow = Q + (size_t)y * nx + xc;
+    // the window column of this lane: plane-major rows (zt == 0) or one z-tiled run (zt > 0, nx a
+    // multiple of 32: xc & 31 is the lane's column in the tile)
+    const F* qrow = zt ? Q + ((size_t)y * (nx >> 5) + (xc >> 5)) * zt * 32 + (xc & 31) : Q + (size_t)y * nx + xc;
+    const size_t zs = zt ? 32 : ps;  // element stride of one window plane
     const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
     F h[RW + 1];
 #pragma unroll
@@ -2394,7 +2421,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         for (int j = 0; j < NJ2; ++j) {
             const int pg = min(w + NW * j, HG - 1);  // surplus slots repeat the last group: equal counts per wave
             const int row = min(RPWI * pg + lane / LPR, H - 1);
-            const F* src = q + (size_t)(clampi(zc0 - RW + row, 0, nz - 1) - zq0) * ps;
+            const F* src = q + (size_t)(clampi(zc0 - RW + row, 0, nz - 1) - zq0) * zs;
             glds16(src, __builtin_amdgcn_readfirstlane(lb + (unsigned)(pg * 1024)));
         }
     };

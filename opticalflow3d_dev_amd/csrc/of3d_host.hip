@@ -72,6 +72,7 @@ struct Knobs {
     bool k5c = true;      // OF3D_K5C=0: k_wz_solve_dma / k_wz_solve instead of K5c
     int k5c_r = 8;        // OF3D_K5C_R=4: 32-plane K5c blocks
     int k5c_nw = 4;       // OF3D_K5C_NW=8: 8-wave, 128-plane K5c blocks
+    bool wxy_tile = true;  // OF3D_WXY_TILE=0: the W-xy hand-off in plain [z][y][x] planes
     bool pipe = true;     // OF3D_PIPE=0: no next-frame K0 inside K5c
     bool general = false;  // OF3D_GENERAL=1: the general-radius path
     int64_t zchunk = 0;   // OF3D_ZCHUNK: overlap mode's z chunk (planes; 0 serial)
@@ -97,6 +98,7 @@ struct Knobs {
         k.k5c = iv("OF3D_K5C", 1) != 0;
         k.k5c_r = iv("OF3D_K5C_R", 8) == 4 ? 4 : 8;
         k.k5c_nw = iv("OF3D_K5C_NW", 4) == 8 ? 8 : 4;
+        k.wxy_tile = iv("OF3D_WXY_TILE", 1) != 0;
         k.pipe = iv("OF3D_PIPE", 1) != 0;
         k.general = iv("OF3D_GENERAL", 0) == 1;
         k.zchunk = std::max(0L, iv("OF3D_ZCHUNK", 0));
@@ -105,7 +107,7 @@ struct Knobs {
     }
     auto tie() const {
         return std::tie(k0c, k1c, k2c, k12, k12_zc, k34, k34_uq, k34_ws, k34_pk, k34_cand, k34_strict, k34_tune, k5c,
-                        k5c_r, k5c_nw, pipe, general, zchunk, verbose);
+                        k5c_r, k5c_nw, wxy_tile, pipe, general, zchunk, verbose);
     }
     bool operator==(const Knobs& o) const { return tie() == o.tie(); }
 };
@@ -118,6 +120,7 @@ struct of3d_plan {
     int64_t nz = 1, ny = 1, nx = 1;
     int rd = 0, rs = 0, rt = 0, rw = 0;
     int device = 0;
+    int ncu = 256;           // compute units of the device (K12 march-length model)
     int64_t cap_planes = 0;  // planes per workspace field
     std::vector<double> htaps;  // host copy of half taps (g | d | s | t | w)
     double* d_taps = nullptr;   // fp64 taps
@@ -135,6 +138,9 @@ struct of3d_plan {
     size_t k5c_lds = 0;
     int k5c_r = 8;  // planes per z-group (8: 64-plane blocks, 2 per CU; 4: 32-plane blocks, 3 per CU)
     const void* k5c_next = nullptr;  // K5c that also forms the next frame's dt0 (frame pipelining)
+    // W-xy hand-off layout (K34 -> K5c, csrc/of3d_dev.hpp wxy_rsrc): 0 plain planes, else z-tiled
+    // [y][x / 32][z][32] with this many planes (cap_planes)
+    int wxy_zt = 0;
     // frame pipelining (of3d_plan_execute_next): the dt0 a previous call formed for these frames
     bool pipe_valid = false;
     const void* pipe_frames[kMaxT] = {};
@@ -461,7 +467,7 @@ int k5c_setup(of3d_plan* p) {
 // planes enough to spread over the 8 XCDs (their halo rows then come from one L2).
 template <typename K, typename F>
 hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int nx, size_t fs, const F* hw,
-                      hipStream_t s, int yb0 = 0, int yb1 = -1) {
+                      hipStream_t s, int zt, int yb0 = 0, int yb1 = -1) {
     if (yb1 < 0) yb1 = ny;
     const int nyo = yb1 - yb0;  // output rows (row-slab plans: the rank's own rows)
     int tx = k.tx, nbx = k.nbx;
@@ -480,7 +486,8 @@ hipError_t launch_k34(const K& k, const F* G, F* P, int ng, int nf, int ny, int 
     const int mb = cpg * nf * k.nbx;
     const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8) * mb);
     void* args[] = {(void*)&G,   (void*)&P,   (void*)&ny,  (void*)&nx,  (void*)&fs,     (void*)&hw,  (void*)&tx,
-                    (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1};
+                    (void*)&nyc, (void*)&nbx, (void*)&nyb, (void*)&cpg, (void*)&groups, (void*)&yb0, (void*)&yb1,
+                    (void*)&zt};
     return hipLaunchKernel(k.fn, dim3(blocks), dim3(k.nthr ? k.nthr : k.cw), args, k.lds, s);
 }
 
@@ -531,7 +538,7 @@ int k34_tune(of3d_plan* p) {
     hipLaunchKernelGGL(k_fill_tune<F>, dim3(2048), dim3(256), 0, p->stream, G, nfill);
     OF3D_HIP(hipGetLastError());
     for (size_t i = 0; i < nc; ++i)  // warm every candidate (code load, caches)
-        OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+        OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream, p->wxy_zt));
     // best of three, the candidates interleaved round-robin (clock drift over the tune hits
     // every candidate alike); each sample two launches back to back, timed together (a single
     // launch after a synchronisation ran up to 5 % off the sustained time of a series: round 5,
@@ -539,10 +546,10 @@ int k34_tune(of3d_plan* p) {
     std::vector<float> ms(nc, 1e30f);
     for (int rep = 0; rep < 3; ++rep) {
         for (size_t i = 0; i < nc; ++i) {
-            OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+            OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream, p->wxy_zt));
             OF3D_HIP(hipEventRecord(e0, p->stream));
             for (int k = 0; k < 2; ++k)
-                OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream));
+                OF3D_HIP(launch_k34(p->k34_cand[i], (const F*)G, P, ng, nf, (int)p->ny, (int)p->nx, p->fs, hw, p->stream, p->wxy_zt));
             OF3D_HIP(hipEventRecord(e1, p->stream));
             OF3D_HIP(hipEventSynchronize(e1));
             float m = 0.f;
@@ -827,11 +834,13 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
     // (LDS-DMA staging: 16-byte rows and planes of dt0 and of the centre frame)
     const bool k12_al = (nx * sizeof(F)) % 16 == 0 && (nx * es) % 16 == 0 &&
                         ((uintptr_t)d_frames[p->rt] + (size_t)(R.zb0 - frame_z0) * plane * es) % 16 == 0;
-    // K12 pays where its blocks can march >= 32 planes and still fill the GPU (c2, 256^2 x 64:
-    // 16-plane marches re-form 12 halo planes each, K1c + K2c measured faster; c3: K12 0.62 vs
-    // 0.83 ms); OF3D_K12=1 forces it, OF3D_K12=0 disables it
+    // K12 pays where its blocks can march >= 32 planes and still fill the GPU: fp64 (one 12-wave
+    // block per CU), one round of 32-plane marches on every CU — c2 (256^2 x 64: 256 blocks) K0
+    // + K12 0.110 ms vs K0 + K1c + K2c 0.142, frame 0.377 vs 0.420 (round 5; with 16-plane
+    // marches 0.126: K1c + K2c had measured faster); fp32, 1024 blocks; c3: K12 0.62 vs 0.83 ms.
+    // OF3D_K12=1 forces it, OF3D_K12=0 disables it
     const int k12_tiles = (int)cdiv(nx, k12_cw<F>() - 2 * p->rd) * (int)cdiv(ny, K12_TY);
-    const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= 1024;
+    const bool k12_big = (long)k12_tiles * cdiv(R.zg1 - R.zg0, 32) >= (sizeof(F) == 8 ? p->ncu : 1024);
     // (fp32 plans, rd <= 6: two blocks per CU — c3 0.27 + 0.36 ms vs K1c + K2c 0.43 + 0.25, c5
     // 12.7 + 21.3 vs 23.5 + 13.2; rd 9 in fp32 runs one block per CU: K1c + K2c)
     const void* k12 = (d3 && p->kn.k12 != 0 && k12_al && plane * sizeof(F) <= 0x7fffffffu &&
@@ -978,11 +987,20 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             // (each march re-forms 2 rd halo planes), at least 16.  Measured: c5 fp32 K12 20.7 /
             // 20.0 / 19.7 ms at 64 / 128 / 256, c4 fp64 4.40 / 4.12 at 64 / 128; c3 keeps 64
             int zc = p->kn.k12_zc;  // OF3D_K12_ZC: forced march length (tests)
-            if (zc <= 0) {
-                zc = 256;
-                // (three full rounds of one block per CU for the 12-wave fp64 blocks)
-                const long kmin = k12_nwx<F>() == 3 ? 768 : 1024;
-                while (zc > 16 && (long)ntile * cdiv(nq, zc) < kmin) zc /= 2;
+            if (zc <= 0 && k12_nwx<F>() == 3) {
+                // fp64 (one 12-wave block per CU): the march with the fewest block-steps on the
+                // busiest CU, rounds of blocks x (march + 2 rd halo steps); ties to the longer
+                // march.  c2: 32 planes (one round of 256 blocks: K12 0.090 ms vs 0.107 at 16 and
+                // 0.107 at 64), c3: 64 (three rounds), c4: 256
+                long best = 0;
+                for (int z = 256; z >= 16; z /= 2) {
+                    const long rounds = cdiv((long)ntile * cdiv(nq, z), std::max(p->ncu, 1));
+                    const long cost = rounds * (std::min(z, nq) + 2 * p->rd);
+                    if (!best || cost < best) best = cost, zc = z;
+                }
+            } else if (zc <= 0) {
+                zc = 256;  // fp32 (two blocks per CU): the longest march with >= 1024 blocks
+                while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;
             }
             const unsigned gx = 8 * cdiv(ntile, 8);
             const size_t lds = k12_lds<F>(dtype, p->rd);
@@ -1023,7 +1041,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
         if (q1 <= q0) return 0;
         const int ng = (int)(q1 - q0);
         const size_t o = (size_t)(q0 - R.zg0) * plane;
-        OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + o, ng, nf, ny, nx, fs, tp.w, st, (int)p->ya, (int)p->yb));
+        // (z-tiled W-xy: plane q0 starts 32 elements per plane in, csrc/of3d_dev.hpp wxy_rsrc)
+        const size_t op = p->wxy_zt ? (size_t)(q0 - R.zg0) * 32 : o;
+        OF3D_HIP(launch_k34(p->k34, Gb + o, Pb + op, ng, nf, ny, nx, fs, tp.w, st, p->wxy_zt, (int)p->ya, (int)p->yb));
         p->used |= p->k34.nthr ? (p->k34.nthr == p->k34.cw ? KU_K34PK : KU_K34WS) : KU_K34;
         return 0;
     };
@@ -1077,7 +1097,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                 int yo0 = (int)p->ya;
                 void* cargs[] = {(void*)&Qc, (void*)&zg0, (void*)&zq1, (void*)&ny,  (void*)&nx,  (void*)&fs,
                                  (void*)&tp.w, (void*)&zoa, (void*)&noa, (void*)&ovx, (void*)&ovy, (void*)&ovz,
-                                 (void*)&orel, (void*)&yo0, (void*)&k0n};
+                                 (void*)&orel, (void*)&yo0, (void*)&k0n, (void*)&p->wxy_zt};
                 OF3D_HIP(hipLaunchKernel(fuse_next ? p->k5c_next : p->k5c, gc, dim3(64 * p->k5c_nw), cargs, p->k5c_lds, st));
                 p->used |= fuse_next ? KU_K5C_NEXT : KU_K5C;
             } else if (p->k5_nb) {
@@ -1242,10 +1262,15 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->device = device;
     if (build_taps(taps, p.get())) return -1;
     OF3D_HIP(hipSetDevice(device));
+    OF3D_HIP(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, device));
     int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
     p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
     p->fs = (size_t)p->cap_planes * ny * nx;
     if (set_attrs(p.get())) return -1;
+    // the z-tiled W-xy hand-off wherever the fused K34 writes it and K5c reads it (nx a multiple
+    // of the 32-column K5c tile)
+    p->wxy_zt = (ndim == 3 && p->kn.wxy_tile && !p->general && p->k34.fn && p->k5c && nx % 32 == 0)
+                    ? (int)p->cap_planes : 0;
     OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
     OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
     {

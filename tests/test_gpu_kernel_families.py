@@ -14,7 +14,7 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_NW", "OF3D_K34_UQ")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_NW", "OF3D_K34_UQ", "OF3D_WXY_TILE")
 
 
 def _run(img, s, t, w, ndim, mode, old, force=None, kernels=None):
@@ -111,6 +111,24 @@ def test_wz_solve_eight_wave_blocks(case, fp32):
     ref = _run(img, s, t, w, ndim, mode, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", range(3))
+@pytest.mark.parametrize("fp32", [False, True])
+def test_wxy_plain_and_tiled_layouts(case, fp32):
+    """The K34 -> K5c hand-off in plain planes (OF3D_WXY_TILE=0) and z-tiled (the default where
+    nx is a multiple of 32; other widths keep the plain layout) against the older kernels:
+    bit-identical.  nx is rounded up to a multiple of 32 here (288, 160, 544)."""
+    shape, (s, t, w), ndim = CASES[case]
+    shape = shape[:-1] + (((shape[-1] + 31) // 32) * 32,)  # nx a multiple of 32: the tiled layout
+    img = np.random.default_rng(660 + case).integers(0, 4096, size=shape).astype(np.uint16)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    tiled = _run(img, s, t, w, ndim, mode, old=False)
+    plain = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_WXY_TILE": "0"})
+    ref = _run(img, s, t, w, ndim, mode, old=True)
+    for a, b, c in zip(tiled, plain, ref):
+        assert a.dtype == c.dtype and np.array_equal(a.view(np.uint8), c.view(np.uint8))
+        assert np.array_equal(b.view(np.uint8), c.view(np.uint8))
 
 
 W_RADII = [
