@@ -821,19 +821,28 @@ __device__ __forceinline__ void buf_st_n(const F (&v)[N], __amdgpu_buffer_rsrc_t
 // window as ONE contiguous run instead of ZC + 2 RW pieces of 256 B a plane apart: the window
 // reads alone take 0.385 instead of 0.488 ms at c3, 3.13 instead of 4.0-4.2 ms at c4
 // (tools/mb_window.hip).  K34 stores per tile of rows from yb: a buffer descriptor at the tile's
-// first element and 32-bit per-lane byte offsets (a tile of S rows spans S nx zt elements).
+// first row and 32-bit per-lane byte offsets (a tile of S rows spans S nx zt elements), through one
+// branch-free formula whose uniform parameters select the layout (a per-store select of the two
+// formulas cost the lockstep K34 36 VGPRs: 3 -> 2 waves per SIMD at c2).
+struct WxyMap {
+    unsigned rs, cm, msk, sh;  // row stride (bytes); column-tile multiplier, mask, shift
+};
 template <typename F>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wxy_rsrc(F* Qp, int zl, int yb, int xo0, int ny, int nx, int zt) {
-    return zt ? buf_rsrc(Qp + ((size_t)yb * nx * zt + (size_t)zl * 32)) : buf_rsrc(Qp + ((size_t)zl * ny + yb) * nx + xo0);
+__device__ __forceinline__ WxyMap wxy_map(int nx, int zt) {
+    constexpr unsigned ES = sizeof(F);
+    return zt ? WxyMap{(unsigned)nx * (unsigned)zt * ES, (unsigned)zt * 32u, 31u, 5u}
+              : WxyMap{(unsigned)nx * ES, 0u, ~0u, 31u};
 }
-// byte offset of row r (of the tile) at column x = xo0 + c0 (c0 + RB - 1 in the same 32-column
-// tile: RB | 32 and xo0 a multiple of RB)
 template <typename F>
-__device__ __forceinline__ unsigned wxy_off(int r, int xo0, int c0, int nx, int zt) {
-    const int x = xo0 + c0;
-    return zt ? ((unsigned)r * (unsigned)nx * (unsigned)zt + (unsigned)(x >> 5) * (unsigned)zt * 32u + (unsigned)(x & 31)) *
-                    (unsigned)sizeof(F)
-              : ((unsigned)r * (unsigned)nx + (unsigned)c0) * (unsigned)sizeof(F);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wxy_rsrc(F* Qp, int zl, int yb, int ny, int nx, int zt) {
+    return zt ? buf_rsrc(Qp + ((size_t)yb * nx * zt + (size_t)zl * 32)) : buf_rsrc(Qp + ((size_t)zl * ny + yb) * nx);
+}
+// byte offset of row r (of the tile) at column x (x .. x + RB - 1 in one 32-column tile: RB | 32 and
+// x a multiple of RB); plain planes: r nx + x (x >> 31 = 0, mask all ones)
+template <typename F>
+__device__ __forceinline__ unsigned wxy_off(const WxyMap& m, int r, int x) {
+    const unsigned ux = (unsigned)x;
+    return (unsigned)r * m.rs + ((ux >> m.sh) * m.cm + (ux & m.msk)) * (unsigned)sizeof(F);
 }
 
 // OCC: waves per SIMD the register budget is cut for (3: 168 VGPRs; 2: 256, for 8-wave blocks,
@@ -914,6 +923,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const auto ra_ = buf_rsrc(G + (size_t)((pa >> (4 * p)) & 15u) * fs + pl);
     const auto rb_ = buf_rsrc(G + (size_t)((pb >> (4 * p)) & 15u) * fs + pl);
     F* const Qp = Q + (size_t)p * fs;
+    const WxyMap wm = wxy_map<F>(nx, zt);
     const unsigned rowb = (unsigned)nx * ES;
     F h[RW + 1];
 #pragma unroll
@@ -946,7 +956,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
     const int nsgw = (nseg + SPW - 1) / SPW;
     auto phase_b = [&](const F* tile, int yb, int nr) {
         lds_barrier();
-        const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
+        const auto rq_ = wxy_rsrc(Qp, zl, yb, ny, nx, zt);
         for (int i = t; i < 64 * RG * nsgw; i += ca) {
             const int l = i & 63, wg = i >> 6;
             const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
@@ -957,7 +967,7 @@ __global__ __launch_bounds__(512, OCC) void k_prod_wyx(const F* __restrict__ G, 
             if (r < nr) {
                 // row offset per lane in voffset (a divergent soffset would be a waterfall loop)
                 const int c0 = RB * sg;
-                const unsigned vo = wxy_off<F>(r, xo0, c0, nx, zt);
+                const unsigned vo = wxy_off<F>(wm, r, xo0 + c0);
                 if (c0 + RB <= txu) {
                     buf_st_n<F, RB>(out, rq_, vo, 0);
                 } else {
@@ -1172,6 +1182,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
     } else {
         const int tb = t - CWA;
         F* const Qp = Q + (size_t)p * fs;
+        const WxyMap wm = wxy_map<F>(nx, zt);
         const int nseg = (txu + RB - 1) / RB;
         constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW;
         constexpr int RG = S / RPW;
@@ -1180,7 +1191,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
             lds_barrier();  // tile tt written
             const F* tile = sw + (tt & 1) * k34_tile(S, cwp);
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
-            const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
+            const auto rq_ = wxy_rsrc(Qp, zl, yb, ny, nx, zt);
             for (int i = tb; i < 64 * RG * nsgw; i += NCT) {
                 const int l = i & 63, wg = i >> 6;
                 const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
@@ -1190,7 +1201,7 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
                 lds_pass_c<RB, RW, DB>(tile + k34_row(r, cwp), 1, RW + RB * sg, h, out);
                 if (r < nr) {
                     const int c0 = RB * sg;
-                    const unsigned vo = wxy_off<F>(r, xo0, c0, nx, zt);
+                    const unsigned vo = wxy_off<F>(wm, r, xo0 + c0);
                     if (c0 + RB <= txu) {
                         buf_st_n<F, RB>(out, rq_, vo, 0);
                     } else {
@@ -1355,6 +1366,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     } else {
         const int tb = t - NPT;
         float* const Qp = Q + (size_t)p * fs;
+        const WxyMap wm = wxy_map<float>(nx, zt);
         const int nseg = (txu + RB - 1) / RB;
         constexpr int PP = S / 2, SPW = 64 / PP;  // pairs per tile; segments per wave item
         const int nsgw = (nseg + SPW - 1) / SPW;
@@ -1362,7 +1374,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
             lds_barrier();  // tile tt written
             const f2* tile = sw + (tt & 1) * TB;
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
-            const auto rq_ = wxy_rsrc(Qp, zl, yb, xo0, ny, nx, zt);
+            const auto rq_ = wxy_rsrc(Qp, zl, yb, ny, nx, zt);
             for (int i = tb; i < 64 * nsgw; i += NPT) {
                 const int l = i & 63, wg = i >> 6;
                 const int pr = l % PP, sg = wg * SPW + l / PP;
@@ -1377,7 +1389,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                         float o[RB];
 #pragma unroll
                         for (int e = 0; e < RB; ++e) o[e] = e2 ? out[e].y : out[e].x;
-                        const unsigned vo = wxy_off<float>(r, xo0, c0, nx, zt);
+                        const unsigned vo = wxy_off<float>(wm, r, xo0 + c0);
                         if (c0 + RB <= txu) {
                             buf_st_n<float, RB>(o, rq_, vo, 0);
                         } else {
@@ -1724,7 +1736,13 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
     F* At = reinterpret_cast<F*>(smem_raw + NSLOT * SLOT);  // [2 buffers][3 fields][even, odd][TY][AP]
     const int t = threadIdx.x, lane = t & 63;
     const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int role = w / NWX, c = 64 * (w % NWX) + lane;
+    // (row role, column part) of wave w, as rp = role * NWX + part: fp64 spreads the roles' work
+    // evenly over the SIMDs (wave w runs on SIMD w % 4; roles 0 / 1 / 2 / 3 do 180 / 180 / 132 /
+    // 104 fp64 ops per step): SIMDs get roles {0,0,3} {1,1,3} {0,2,3} {1,2,2} instead of {0,1,2}
+    // {0,1,3} {0,2,3} {1,2,3} (busiest SIMD 464 instead of 492 ops per step).  Same box: c3 K12
+    // 0.445 / 0.447 -> 0.435 / 0.438 ms, c4 3.26 -> 3.22, c2 0.089 -> 0.087 (profiles/r05/ab_k12_perm/)
+    const int rp = NWX == 3 ? (int)((0x8ba976415230ull >> (4 * w)) & 15u) : w;
+    const int role = rp / NWX, c = 64 * (rp % NWX) + lane;
     const int per = (ntile + 7) >> 3;
     const int tile = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     if (tile >= ntile) return;  // block-uniform

@@ -72,7 +72,7 @@ struct Knobs {
     bool k5c = true;      // OF3D_K5C=0: k_wz_solve_dma / k_wz_solve instead of K5c
     int k5c_r = 8;        // OF3D_K5C_R=4: 32-plane K5c blocks
     int k5c_nw = 4;       // OF3D_K5C_NW=8: 8-wave, 128-plane K5c blocks
-    bool wxy_tile = true;  // OF3D_WXY_TILE=0: the W-xy hand-off in plain [z][y][x] planes
+    int wxy_tile = -1;    // OF3D_WXY_TILE=0 / 1: the W-xy hand-off in plain planes / z-tiled (-1: by size)
     bool pipe = true;     // OF3D_PIPE=0: no next-frame K0 inside K5c
     bool general = false;  // OF3D_GENERAL=1: the general-radius path
     int64_t zchunk = 0;   // OF3D_ZCHUNK: overlap mode's z chunk (planes; 0 serial)
@@ -98,7 +98,7 @@ struct Knobs {
         k.k5c = iv("OF3D_K5C", 1) != 0;
         k.k5c_r = iv("OF3D_K5C_R", 8) == 4 ? 4 : 8;
         k.k5c_nw = iv("OF3D_K5C_NW", 4) == 8 ? 8 : 4;
-        k.wxy_tile = iv("OF3D_WXY_TILE", 1) != 0;
+        k.wxy_tile = (int)iv("OF3D_WXY_TILE", -1);
         k.pipe = iv("OF3D_PIPE", 1) != 0;
         k.general = iv("OF3D_GENERAL", 0) == 1;
         k.zchunk = std::max(0L, iv("OF3D_ZCHUNK", 0));
@@ -1268,8 +1268,12 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     p->fs = (size_t)p->cap_planes * ny * nx;
     if (set_attrs(p.get())) return -1;
     // the z-tiled W-xy hand-off wherever the fused K34 writes it and K5c reads it (nx a multiple
-    // of the 32-column K5c tile)
-    p->wxy_zt = (ndim == 3 && p->kn.wxy_tile && !p->general && p->k34.fn && p->k5c && nx % 32 == 0)
+    // of the 32-column K5c tile), for fp64 workspaces of >= 128 planes: K5c's contiguous windows
+    // gain more there than K34's 256-byte store pieces cost (same box, tiled vs planes: c3 frame
+    // 3.164 / 3.151 vs 3.175 / 3.183 ms, c4 21.58 vs 21.98; c2 (64 planes) 0.389 / 0.387 vs 0.381 /
+    // 0.385, c5 fp32 (128-byte pieces) 102.5 vs 102.1: planes there; profiles/r05/ab_wxy_tile2/)
+    p->wxy_zt = (ndim == 3 && p->kn.wxy_tile != 0 && !p->general && p->k34.fn && p->k5c && nx % 32 == 0 &&
+                 (p->kn.wxy_tile == 1 || (!p->fp32 && p->cap_planes >= 128)))
                     ? (int)p->cap_planes : 0;
     OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
     OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));

@@ -195,7 +195,8 @@ def test_c3_fp32_plans_vs_oracle_and_candidates(c3):
     mode = _lib.OF3D_FP32
     ref, _ = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
     ncand = k34_candidates(d_in, p, mode)
-    for v in [dict(OF3D_K34_CAND=i) for i in range(ncand)] + [dict(OF3D_K12=0), dict(OF3D_K5C_R=4)]:
+    for v in [dict(OF3D_K34_CAND=i) for i in range(ncand)] + [dict(OF3D_K12=0), dict(OF3D_K5C_R=4),
+                                                               dict(OF3D_WXY_TILE=1)]:
         with env(**v):
             outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
         for a, b, name in zip(ref, outs, ("vx", "vy", "vz", "rel")):

@@ -116,14 +116,14 @@ def test_wz_solve_eight_wave_blocks(case, fp32):
 @pytest.mark.parametrize("case", range(3))
 @pytest.mark.parametrize("fp32", [False, True])
 def test_wxy_plain_and_tiled_layouts(case, fp32):
-    """The K34 -> K5c hand-off in plain planes (OF3D_WXY_TILE=0) and z-tiled (the default where
-    nx is a multiple of 32; other widths keep the plain layout) against the older kernels:
-    bit-identical.  nx is rounded up to a multiple of 32 here (288, 160, 544)."""
+    """The K34 -> K5c hand-off in plain planes (OF3D_WXY_TILE=0) and z-tiled (OF3D_WXY_TILE=1; the
+    default for fp64 workspaces of >= 128 planes with nx a multiple of 32) against the older
+    kernels: bit-identical.  nx is rounded up to a multiple of 32 here (288, 160, 544)."""
     shape, (s, t, w), ndim = CASES[case]
     shape = shape[:-1] + (((shape[-1] + 31) // 32) * 32,)  # nx a multiple of 32: the tiled layout
     img = np.random.default_rng(660 + case).integers(0, 4096, size=shape).astype(np.uint16)
     mode = _lib.OF3D_FP32 if fp32 else 0
-    tiled = _run(img, s, t, w, ndim, mode, old=False)
+    tiled = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_WXY_TILE": "1"})
     plain = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_WXY_TILE": "0"})
     ref = _run(img, s, t, w, ndim, mode, old=True)
     for a, b, c in zip(tiled, plain, ref):
