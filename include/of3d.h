@@ -123,9 +123,11 @@ int of3d_flow2d(const void* images, int dtype, int64_t nt, int64_t ny, int64_t n
 
 /* ---- device-resident plan (streaming driver, benchmarks, z-slab shards) -- */
 
-/* ndim 3: volume (nz, ny, nx); ndim 2: nz must be 1.  Allocates the device
- * workspace on `device` for outputs over up to `max_out_planes` planes
- * (<= 0: all nz). */
+/* ndim 3: volume (nz, ny, nx); ndim 2: nz independent 2D frames processed
+ * together (a batch of output frames: plane b of every frame pointer is the
+ * image of window b, e.g. a series shifted by 0 .. 2rt frames; nz = 1 is
+ * calc_flow2D's single frame).  Allocates the device workspace on `device`
+ * for outputs over up to `max_out_planes` planes (<= 0: all nz). */
 int of3d_plan_create(of3d_plan** plan, int ndim, int64_t nz, int64_t ny, int64_t nx,
                      const of3d_taps* taps, int mode, int device, int64_t max_out_planes);
 int of3d_plan_destroy(of3d_plan* plan);

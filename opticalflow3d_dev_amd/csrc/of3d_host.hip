@@ -640,9 +640,9 @@ Ranges ranges(const of3d_plan* p, int64_t zo0, int64_t zo1) {
     Ranges r;
     r.zo0 = zo0;
     r.zo1 = zo1;
-    if (p->ndim == 2) {
-        r.zg0 = r.zb0 = 0;
-        r.zg1 = r.zb1 = 1;
+    if (p->ndim == 2) {  // planes = independent frames of a batch: no halo
+        r.zg0 = r.zb0 = zo0;
+        r.zg1 = r.zb1 = zo1;
         return r;
     }
     r.zg0 = std::max<int64_t>(zo0 - p->rw, 0);
@@ -730,8 +730,8 @@ int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, con
         Gr = X;
         gz0 = zg0, gz1 = zg1;
     } else {
-        Gr = Y + 2 * fs;  // dt, dy, dx
-        gz0 = 0, gz1 = 1;
+        Gr = Y + 2 * fs;  // dt, dy, dx (2D: the batch's planes, origin zb0 = zg0)
+        gz0 = zg0, gz1 = zg1;
     }
     if (mark(2)) return -1;
     const int np = d3 ? 9 : 5;
@@ -758,8 +758,9 @@ int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, con
             hipLaunchKernelGGL((k_solve3_gen<F, float>), grid(n), dim3(256), 0, st, (const F*)X, fs, n, vx, vy, vz,
                                (float*)rel);
     } else {
-        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv((int64_t)plane, 256)), dim3(256), 0, st, (const F*)Pp, fs,
-                           (int)plane, vx, vy, (F*)rel);
+        const int64_t n = (int64_t)(zo1 - zo0) * (int64_t)plane;
+        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st, (const F*)Pp, fs, (int)n, vx, vy,
+                           (F*)rel);
     }
     OF3D_HIP(hipGetLastError());
     return mark(5);
@@ -1110,8 +1111,10 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                 p->used |= KU_K5;
             }
         } else {
-            const int n = ny * nx;
-            hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st, (const F*)Qb, fs, n, vx, vy, (F*)rel);
+            // (2D: planes [o0, o1) of a batch of independent frames)
+            const int n = (int)(o1 - o0) * ny * nx;
+            hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st,
+                               (const F*)Qb + (size_t)(o0 - R.zg0) * plane, fs, n, ovx, ovy, (F*)orel);
             p->used |= KU_SOLVE2D;
         }
         OF3D_HIP(hipGetLastError());
@@ -1239,7 +1242,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     *out = nullptr;
     if ((mode & ~(OF3D_REL_F64 | OF3D_FP32)) != OF3D_FP64_EXACT) return fail("of3d: unsupported mode");
     if (ndim != 2 && ndim != 3) return fail("of3d: ndim must be 2 or 3");
-    if (ndim == 2 && nz != 1) return fail("of3d: 2D plans need nz == 1");
+    // (2D: nz independent frames processed together — a batch of output frames; no coupling)
     if (nz < 1 || ny < 1 || nx < 1) return fail("of3d: empty volume");
     if (ny * nx > (int64_t)INT32_MAX || nz > 65535) return fail("of3d: volume too large for one plan");
     // every error path below frees whatever the plan holds so far (plan_free takes partial plans)
@@ -1264,7 +1267,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     OF3D_HIP(hipSetDevice(device));
     OF3D_HIP(hipDeviceGetAttribute(&p->ncu, hipDeviceAttributeMultiprocessorCount, device));
     int64_t mo = (max_out_planes <= 0 || max_out_planes > nz) ? nz : max_out_planes;
-    p->cap_planes = ndim == 2 ? 1 : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
+    p->cap_planes = ndim == 2 ? mo : std::min<int64_t>(nz, mo + 2 * (p->rw + p->rd));
     p->fs = (size_t)p->cap_planes * ny * nx;
     if (set_attrs(p.get())) return -1;
     // the z-tiled W-xy hand-off wherever the fused K34 writes it and K5c reads it (nx a multiple
