@@ -113,3 +113,20 @@ def test_overlap_and_row_range_exclude_each_other():
             plan.set_rows(5, 30)
     finally:
         plan.close()
+
+
+@pytest.mark.parametrize("chunk", [8, 13])
+def test_overlap_z_tiled_bitwise(chunk, monkeypatch):
+    """Overlap mode with the z-tiled W-xy hand-off forced (OF3D_WXY_TILE=1, nx 64): every chunk's
+    K34 writes its planes 32 elements per plane into the tiles (csrc/of3d_host.hip k34 lambda) and
+    K5c reads them back — bit-identical to the serial pipeline in plain planes."""
+    s, t, w = 2, 2, 5
+    img = np.random.default_rng(70 + chunk).integers(0, 4096, size=(13, 48, 40, 64)).astype(np.uint16)
+    monkeypatch.setenv("OF3D_WXY_TILE", "0")
+    serial, _ = _run_plan(img, s, t, w, 0)
+    monkeypatch.setenv("OF3D_WXY_TILE", "1")
+    over, _ = _run_plan(img, s, t, w, chunk)
+    sub, _ = _run_plan(img, s, t, w, chunk, z0=10, z1=38)
+    for a, b, c in zip(serial, over, sub):
+        assert bits_equal(a, b)
+        assert bits_equal(a[10:38], c)

@@ -138,3 +138,43 @@ def test_plan_output_rows(rows, fp32):
     part = run(ya, yb)
     for a, b in zip(full, part):
         assert np.array_equal(a[:, ya:yb].view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("rows", [(7, 41), (59, 60), (0, 60)])
+@pytest.mark.parametrize("fp32", [False, True])
+def test_plan_output_rows_z_tiled(rows, fp32, monkeypatch):
+    """of3d_plan_set_rows with the z-tiled W-xy hand-off forced (OF3D_WXY_TILE=1; nx a multiple of
+    32): the rows K34 writes and K5c reads in the tiled layout, bit-identical to the plain-plane
+    whole-plane outputs."""
+    import torch
+
+    ya, yb = rows
+    nz, ny, nx = 20, 60, 64
+    img = np.random.default_rng(12).integers(0, 4096, size=(13, nz, ny, nx)).astype(np.uint16)
+    s, t, w = 2, 2, 5
+    rt = radii(s, t, w)[2]
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(np.ascontiguousarray(img[6 - rt:6 + rt + 1]).view(np.int16)).to(dev)
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    vt = torch.float32 if fp32 else torch.float64
+
+    def run(r0, r1, tile):
+        monkeypatch.setenv("OF3D_WXY_TILE", tile)
+        plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=0, mode=mode)
+        try:
+            if (r0, r1) != (0, ny):
+                plan.set_rows(r0, r1)
+            n = nz * (r1 - r0) * nx
+            outs = [torch.empty(n, dtype=vt, device=dev) for _ in range(3)] + [torch.empty(n, dtype=torch.float32,
+                                                                                          device=dev)]
+            plan.execute([d_in[i].data_ptr() for i in range(2 * rt + 1)], _lib.OF3D_U16, 0, 0, nz,
+                         *[o.data_ptr() for o in outs])
+            torch.cuda.synchronize(dev)
+            return [o.cpu().numpy().reshape(nz, r1 - r0, nx) for o in outs]
+        finally:
+            plan.close()
+
+    full = run(0, ny, "0")
+    part = run(ya, yb, "1")
+    for a, b in zip(full, part):
+        assert np.array_equal(a[:, ya:yb].view(np.uint8), b.view(np.uint8))
