@@ -2366,6 +2366,12 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
 }
 
 constexpr int K5C_G = 4;  // voxels per straight-line group in K5c's epilogue (k5_solve_store)
+// LDS-read distance of K5c's W z passes (lds_pass_c's D: window values read D taps ahead).  fp64:
+// 3 (c3 K5c 0.993 / 0.994 -> 0.979 / 0.974 ms over four same-box pairs, c4 6.80 -> 6.75; 4: c3
+// 0.98, c4 slower; the VGPR count stays 206, set by the epilogue); fp32 keeps 2 (c5: 36.0 vs
+// 36.1 ms).  profiles/r05/ab_k5c_d/
+template <typename F>
+constexpr int K5C_D = sizeof(F) == 8 ? 3 : 2;
 
 // K5c block coordinates from the launch's (columns, rows, z chunks) grid, XCD-aware: the
 // linear workgroup id b runs on XCD b % 8, so the z chunks of one (column block, row) — whose
@@ -2477,7 +2483,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         else
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (f + NB - 1 < 9) issue(f + NB - 1, (f + NB - 1) % NB);
-        lds_pass_c<R, RW, 2>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
+        lds_pass_c<R, RW, K5C_D<F>>(sm + (f % NB) * HG * RPWI * CB + col, CB, RW + gz * R, h, acc[f]);
         // pin the pass here: without it the compiler sinks every field's arithmetic below the
         // last barrier and keeps all 9 windows' LDS reads live in registers (spills)
 #pragma unroll
