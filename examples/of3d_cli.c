@@ -64,7 +64,10 @@ int main(int argc, char** argv) {
     size_t ni = 0, nt_ = 0;
     uint16_t* img = (uint16_t*)read_file(argv[1], &ni);
     double* tp = (double*)read_file(argv[6], &nt_);
-    if (!img || !tp || ni != (size_t)(nt * nz * ny * nx) * sizeof(uint16_t) || nt_ < 4 * sizeof(double)) {
+    /* the stack's size as a quotient (no product of nt that could overflow): whole volumes of
+       nz * ny * nx uint16 (ny * nx <= INT32_MAX and nz <= 65535, so that product fits), and exactly nt */
+    const uint64_t vol_bytes = (uint64_t)nz * (uint64_t)(ny * nx) * sizeof(uint16_t);
+    if (!img || !tp || ni % vol_bytes != 0 || ni / vol_bytes != (uint64_t)nt || nt_ < 4 * sizeof(double)) {
         fprintf(stderr, "of3d_cli: bad input files\n");
         return 2;
     }

@@ -225,6 +225,13 @@ int of3d_plan_set_rows(of3d_plan* plan, int64_t y0, int64_t y1);
 int of3d_plan_kernels(const of3d_plan* plan, char* buf, size_t n);
 const char* of3d_stage_name(int i);
 
+/* The plan's kernel geometry as a JSON object, written like of3d_plan_kernels (returns the
+ * full length): the W-xy hand-off layout (wxy_zt: 0 plain planes, else z-tiled), the K34 shape
+ * the autotune kept (staged columns, tile rows s, outputs per block, threads, candidates), the K5c
+ * block (planes per z-group, waves), and of the LAST execution the K12 march length and grid and
+ * the batched-K0 windows.  Diagnostics for tests and benchmarks (no reference counterpart). */
+int of3d_plan_geometry(const of3d_plan* plan, char* buf, size_t n);
+
 /* Copy `bytes` from src to dst on `stream` with a kernel of at most
  * `max_blocks` workgroups (0 = 64).  Either side may be pinned host memory
  * (hipHostMalloc / torch pin_memory): used to download a frame's outputs

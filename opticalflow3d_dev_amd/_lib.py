@@ -8,6 +8,7 @@ library is missing or no GPU is visible, calls raise loudly.
 from __future__ import annotations
 
 import ctypes
+import json
 import os
 import threading
 
@@ -39,7 +40,7 @@ EXPORTED = (
     "of3d_copy_async", "of3d_dma_copy", "of3d_plan_set_timing_mask", "of3d_flow_stats",
     "of3d_plan_set_overlap", "of3d_cache_clear", "of3d_plan_set_rows",
     "of3d_plan_kernels", "of3d_build_info", "of3d_plan_execute_next", "of3d_plan_execute_ahead",
-    "of3d_rel3d",
+    "of3d_rel3d", "of3d_plan_geometry",
 )
 
 CSRC = os.path.join(_HERE, "csrc")
@@ -187,6 +188,8 @@ def load():
         lib.of3d_plan_set_rows.restype = ctypes.c_int
         lib.of3d_plan_kernels.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
         lib.of3d_plan_kernels.restype = ctypes.c_int
+        lib.of3d_plan_geometry.argtypes = [P, ctypes.c_char_p, ctypes.c_size_t]
+        lib.of3d_plan_geometry.restype = ctypes.c_int
         d = ctypes.c_double
         lib.of3d_flow_stats.argtypes = [P, P, P, P, ctypes.c_int, ctypes.c_int, i64, d, d, d, d, P, P, P, P, P, P, P]
         lib.of3d_flow_stats.restype = ctypes.c_int
@@ -315,6 +318,14 @@ class Plan:
         buf = ctypes.create_string_buffer(n + 1)
         check(self.lib.of3d_plan_kernels(self.handle, buf, n + 1))
         return [k for k in buf.value.decode().split(",") if k]
+
+    def geometry(self):
+        """of3d_plan_geometry: the plan's kernel shapes (W-xy layout, K34, K5c) and the last
+        execution's K12 march / batched-K0 windows, as a dict."""
+        n = check(self.lib.of3d_plan_geometry(self.handle, None, 0))
+        buf = ctypes.create_string_buffer(n + 1)
+        check(self.lib.of3d_plan_geometry(self.handle, buf, n + 1))
+        return json.loads(buf.value.decode())
 
     def set_timing_stages(self, names=None):
         """Time only these stages (None: all); fewer events, less perturbation."""

@@ -2587,11 +2587,11 @@ __global__ __launch_bounds__(256) void k_solve3_gen(const F* __restrict__ W, siz
 }
 
 // 2D (calc_flow.py:154-168). field order: tx ty xy x2 y2
+// (grid-stride over a 64-bit count: a 2D batch plan may hold more than 2^31 pixels)
 template <typename F>
-__global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t fs, int n, F* __restrict__ vx,
+__global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t fs, size_t n, F* __restrict__ vx,
                                                  F* __restrict__ vy, F* __restrict__ rel) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     const double tx = Q[i], ty = Q[fs + i], xy = Q[2 * fs + i], x2 = Q[3 * fs + i], y2 = Q[4 * fs + i];
     const double det = (x2 * y2) - (xy * xy);
     const double R = 1.0 / (det + kEps);
@@ -2603,6 +2603,7 @@ __global__ __launch_bounds__(256) void k_solve2d(const F* __restrict__ Q, size_t
     const double L2 = (tr - sqrt(disc)) / 2.0;
     // np.minimum propagates NaN
     rel[i] = (F)((L1 != L1) ? L1 : ((L2 != L2) ? L2 : (L1 < L2 ? L1 : L2)));
+    }
 }
 
 // ---------------------------------------------------------------------------

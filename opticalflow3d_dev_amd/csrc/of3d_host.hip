@@ -160,6 +160,9 @@ struct of3d_plan {
     int k5c_nw = 4;       // K5c waves per block (8: 128-plane blocks)
     int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
     unsigned used = 0;       // kernel families launched so far (KU_* bits, of3d_plan_kernels)
+    // geometry of the last execution (of3d_plan_geometry): K12 march length and grid, K0 windows
+    int last_k12_zc = 0, last_k12_gx = 0, last_k12_gy = 0, last_k0m = 0;
+    hipEvent_t ev_done = nullptr;  // recorded on the caller's stream at the end of every execution
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
         const void* fn = nullptr;
@@ -758,9 +761,9 @@ int run_general(of3d_plan* p, const Frames& fr, int dtype, int64_t frame_z0, con
             hipLaunchKernelGGL((k_solve3_gen<F, float>), grid(n), dim3(256), 0, st, (const F*)X, fs, n, vx, vy, vz,
                                (float*)rel);
     } else {
-        const int64_t n = (int64_t)(zo1 - zo0) * (int64_t)plane;
-        hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st, (const F*)Pp, fs, (int)n, vx, vy,
-                           (F*)rel);
+        const size_t n = (size_t)(zo1 - zo0) * plane;
+        hipLaunchKernelGGL(k_solve2d<F>, dim3((unsigned)std::min<size_t>((n + 255) / 256, 256 * 64)), dim3(256), 0, st,
+                           (const F*)Pp, fs, n, vx, vy, (F*)rel);
     }
     OF3D_HIP(hipGetLastError());
     return mark(5);
@@ -902,6 +905,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             void* margs[] = {(void*)&frm, (void*)&off0, (void*)&ng, (void*)&tp.t, (void*)&D0, (void*)&dstride};
             OF3D_HIP(hipLaunchKernel(k0m_k, dim3(blocks), dim3(256), margs, 0, st));
             p->used |= KU_K0M;
+            p->last_k0m = k0m;
         } else if (!skip_k0) {  // (else: dt0 formed by an earlier call: K5c's next / a batched K0)
             long long fstride = 0;
             if (nwin > 1) {
@@ -1010,6 +1014,7 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                             (void*)&nbx};
             OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(k12_threads<F>()), args, lds, st));
             p->used |= KU_K12;
+            p->last_k12_zc = zc, p->last_k12_gx = (int)gx, p->last_k12_gy = (int)cdiv(nq, zc);
             return 0;
         }
         const void* k2c = nullptr;
@@ -1112,9 +1117,9 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
             }
         } else {
             // (2D: planes [o0, o1) of a batch of independent frames)
-            const int n = (int)(o1 - o0) * ny * nx;
-            hipLaunchKernelGGL(k_solve2d<F>, dim3(cdiv(n, 256)), dim3(256), 0, st,
-                               (const F*)Qb + (size_t)(o0 - R.zg0) * plane, fs, n, ovx, ovy, (F*)orel);
+            const size_t n = (size_t)(o1 - o0) * plane;  // (64-bit: a batch may exceed 2^31 pixels)
+            hipLaunchKernelGGL(k_solve2d<F>, dim3((unsigned)std::min<size_t>((n + 255) / 256, 256 * 64)), dim3(256), 0,
+                               st, (const F*)Qb + (size_t)(o0 - R.zg0) * plane, fs, n, ovx, ovy, (F*)orel);
             p->used |= KU_SOLVE2D;
         }
         OF3D_HIP(hipGetLastError());
@@ -1230,11 +1235,26 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
 int run(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0, int64_t zo0, int64_t zo1, void* vx,
         void* vy, void* vz, void* rel, hipStream_t s, const void* const* d_next = nullptr, bool pipe = false,
         int ahead = -1) {
-    return p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead)
-                   : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead);
+    const int rc = p->fp32 ? run_t<float>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead)
+                           : run_t<double>(p, d_frames, dtype, frame_z0, zo0, zo1, vx, vy, vz, rel, s, d_next, pipe, ahead);
+    // completion marker: plan_free waits for the plan's own work only (not the whole device)
+    if (rc == 0 && p->ev_done) OF3D_HIP(hipEventRecord(p->ev_done, s));
+    return rc;
 }
 
 void plan_free(of3d_plan* p);
+
+// The z-tiled W-xy layout addresses a K34 tile of S rows through ONE buffer descriptor with 32-bit
+// byte offsets (csrc/of3d_dev.hpp wxy_rsrc / wxy_off): S * nx * cap_planes elements must stay below
+// 2^31 bytes for the largest S of any K34 candidate the autotune may pick (an fp64 plan
+// of nz = nx = 4096, ny = 64 would span 2 GiB per 16-row tile, and stores past it are dropped by the
+// descriptor's range check without an error).  Plans past it keep the plain planes.
+bool wxy_tile_fits(const of3d_plan* p) {
+    int smax = p->k34.s;
+    for (const auto& k : p->k34_cand) smax = std::max(smax, k.s);
+    const size_t es = p->fp32 ? sizeof(float) : sizeof(double);
+    return (size_t)smax * (size_t)p->nx * (size_t)p->cap_planes * es <= 0x7fffffffu;
+}
 
 int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, const of3d_taps* taps, int mode,
                 int device, int64_t max_out_planes) {
@@ -1276,7 +1296,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
     // 3.164 / 3.151 vs 3.175 / 3.183 ms, c4 21.58 vs 21.98; c2 (64 planes) 0.389 / 0.387 vs 0.381 /
     // 0.385, c5 fp32 (128-byte pieces) 102.5 vs 102.1: planes there; profiles/r05/ab_wxy_tile2/)
     p->wxy_zt = (ndim == 3 && p->kn.wxy_tile != 0 && !p->general && p->k34.fn && p->k5c && nx % 32 == 0 &&
-                 (p->kn.wxy_tile == 1 || (!p->fp32 && p->cap_planes >= 128)))
+                 (p->kn.wxy_tile == 1 || (!p->fp32 && p->cap_planes >= 128)) && wxy_tile_fits(p.get()))
                     ? (int)p->cap_planes : 0;
     OF3D_HIP(hipMalloc(&p->d_taps, p->htaps.size() * sizeof(double)));
     OF3D_HIP(hipMemcpy(p->d_taps, p->htaps.data(), p->htaps.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -1311,6 +1331,7 @@ int plan_create(of3d_plan** out, int ndim, int64_t nz, int64_t ny, int64_t nx, c
         if ((p->fp32 ? k34_tune<float>(p.get()) : k34_tune<double>(p.get()))) return -1;
     }
     for (auto& e : p->ev) OF3D_HIP(hipEventCreate(&e));
+    OF3D_HIP(hipEventCreateWithFlags(&p->ev_done, hipEventDisableTiming));
     *out = p.release();
     return 0;
 }
@@ -1319,7 +1340,12 @@ void plan_free(of3d_plan* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
-    (void)hipDeviceSynchronize();  // executions on callers' streams may still read the workspace
+    // executions on callers' streams may still read the workspace: wait for the last one (every
+    // execution records ev_done on its stream; a plan's executions are ordered by its caller, as
+    // they share the workspace) — not for the whole device, which would also wait for unrelated
+    // streams while the host-entry cache holds its lock
+    if (p->ev_done) (void)hipEventSynchronize(p->ev_done);
+    else (void)hipDeviceSynchronize();  // (a partial plan: no event yet)
     (void)hipFree(p->d_taps);
     (void)hipFree(p->d_taps32);
     (void)hipFree(p->X);
@@ -1338,6 +1364,7 @@ void plan_free(of3d_plan* p) {
         (void)hipStreamDestroy(p->stream2);
     }
     if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (p->ev_done) (void)hipEventDestroy(p->ev_done);
     delete p;
 }
 
@@ -1385,6 +1412,13 @@ int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, i
     const int64_t c = nt / 2;  // ceil(Nt/2)-1 for odd Nt (calc_flow.py:223)
     const int rt = taps->rt;
     if (taps->rt < 0 || 2 * rt + 1 > kMaxT) return fail("of3d: temporal tap radius exceeds 32");
+    // plans evicted from the cache are freed after the lock is released (declared before it)
+    struct Evicted {
+        std::vector<of3d_plan*> v;
+        ~Evicted() {
+            for (of3d_plan* q : v) plan_free(q);
+        }
+    } evicted;
     std::lock_guard<std::mutex> lk(g_cache_mu);
     CacheKey key = make_key(ndim, device, mode, nz, ny, nx, taps);
     of3d_plan* p = nullptr;
@@ -1398,7 +1432,7 @@ int host_flow(int ndim, const void* images, int dtype, int64_t nt, int64_t nz, i
         if (plan_create(&p, ndim, nz, ny, nx, taps, mode, device, 0)) return -1;
         g_cache.insert(g_cache.begin(), CacheEntry{key, p});
         while (g_cache.size() > 2) {
-            plan_free(g_cache.back().plan);
+            evicted.v.push_back(g_cache.back().plan);
             g_cache.pop_back();
         }
     }
@@ -1655,6 +1689,29 @@ int of3d_plan_kernels(const of3d_plan* p, char* buf, size_t n) {
     std::string out;
     for (size_t i = 0; i < sizeof(kKernelNames) / sizeof(kKernelNames[0]); ++i)
         if ((p->used >> i) & 1u) out += (out.empty() ? "" : ",") + std::string(kKernelNames[i]);
+    if (buf && n) {
+        const size_t k = std::min(n - 1, out.size());
+        memcpy(buf, out.data(), k);
+        buf[k] = 0;
+    }
+    return (int)out.size();
+}
+
+int of3d_plan_geometry(const of3d_plan* p, char* buf, size_t n) {
+    if (!p) return fail("of3d: null plan");
+    int smax = p->k34.s;
+    for (const auto& k : p->k34_cand) smax = std::max(smax, k.s);
+    char tmp[768];
+    snprintf(tmp, sizeof(tmp),
+             "{\"ndim\": %d, \"nz\": %lld, \"ny\": %lld, \"nx\": %lld, \"fp32\": %d, \"general\": %d, "
+             "\"cap_planes\": %lld, \"wxy_zt\": %d, \"k34\": {\"cw\": %d, \"s\": %d, \"tx\": %d, \"nbx\": %d, "
+             "\"threads\": %d, \"lds\": %zu, \"candidates\": %zu, \"s_max\": %d}, \"k5c\": {\"r\": %d, \"nw\": %d, "
+             "\"lds\": %zu}, \"k12\": {\"march\": %d, \"grid\": [%d, %d]}, \"k0_batch\": %d, \"ncu\": %d}",
+             p->ndim, (long long)p->nz, (long long)p->ny, (long long)p->nx, (int)p->fp32, (int)p->general,
+             (long long)p->cap_planes, p->wxy_zt, p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx,
+             p->k34.nthr ? p->k34.nthr : p->k34.cw, p->k34.lds, p->k34_cand.size(), smax, p->k5c ? p->k5c_r : 0,
+             p->k5c ? p->k5c_nw : 0, p->k5c_lds, p->last_k12_zc, p->last_k12_gx, p->last_k12_gy, p->last_k0m, p->ncu);
+    const std::string out(tmp);
     if (buf && n) {
         const size_t k = std::min(n - 1, out.size());
         memcpy(buf, out.data(), k);

@@ -92,3 +92,26 @@ def test_batch_plan_general_path():
     assert "general" in kernels, kernels
     for a, b in zip(ref, gen):
         assert _same(b, a)
+
+
+def test_c1_full_series_batch_plan_vs_oracle():
+    """configs[0] exactly as bench.py --config c1 times it: a 16-frame 256 x 256 series (the bench's
+    synthetic family and seed), xySig 1, tSig 1, wSig 5 — one 2D plan of 10 planes over the series
+    shifted by 0 .. 6 frames, so plane b is output frame b — then every one of the 10 output frames
+    bitwise (vx, vy, rel) against the oracle's calc_flow2D of its own 7-frame window."""
+    import torch
+
+    import bench
+
+    s, t, w = 1, 1, 5
+    nt, ny, nx = 16, 256, 256
+    dev = torch.device("cuda", 0)
+    series = bench.synthetic_slab(nt, 1, ny, nx, 0, 1, 20260206 + 1, dev).view(nt, ny, nx).cpu().numpy()
+    series = series.view(np.uint16)
+    outs, kernels, nwin = _batch(series, s, t, w)
+    assert nwin == 7 and outs[0].shape == (nt - nwin + 1, ny, nx)
+    assert "k_solve2d" in kernels, kernels
+    for j in range(nt - nwin + 1):
+        want = cpu_ref.calc_flow2D(series[j:j + nwin], s, t, w, backend="scipy")
+        for o, a, name in zip(outs, want, ("vx", "vy", "rel")):
+            assert _same(o[j], a), (j, name)

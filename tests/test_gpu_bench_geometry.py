@@ -245,10 +245,10 @@ def long_volume():
 
 
 @pytest.mark.parametrize("fp32", [False, True])
-@pytest.mark.parametrize("zc", [128, 256])
+@pytest.mark.parametrize("zc", [32, 128, 256])
 def test_k12_long_marches_vs_oracle(long_volume, zc, fp32):
-    """OF3D_K12_ZC = 128 / 256 (the c4 / c5 marches) against the full oracle: fp64 bitwise,
-    fp32 within 1e-4 max|v| and bit-identical to the 16-plane marches of the same plan."""
+    """OF3D_K12_ZC = 32 / 128 / 256 (the c2 / c4 / c5 marches) against the full oracle: fp64
+    bitwise, fp32 within 1e-4 max|v| and bit-identical to the 16-plane marches of the same plan."""
     from opticalflow3d_dev_amd import _lib
 
     d_in, (vx, vy, vz, lmin, lmax) = long_volume
@@ -337,3 +337,22 @@ def test_c4_shaped_plan_every_k34_candidate(fp32):
     for box in ((4, 20, 24, 40, 330, 360), (4, 20, 24, 40, 500, 530), (4, 20, 24, 40, 676, 700),
                 (4, 20, 40, 64, 0, 24), (0, 16, 0, 20, 1000, 1024)):
         crop_check(host_in, ref, box, p["s"], p["t"], p["w"], fp32=fp32)
+
+
+@pytest.mark.parametrize("nz,tiled", [(4096, True), (32768, False)])
+def test_wxy_tiled_layout_size_guard(nz, tiled):
+    """The z-tiled W-xy hand-off addresses a K34 tile of S rows through one buffer descriptor with
+    32-bit offsets: a plan whose S_max * nx * cap_planes * 8 bytes would pass 2^31 keeps the plain
+    planes even when tiling is forced (OF3D_WXY_TILE=1), one that fits takes the tiles (ADVICE r05;
+    csrc/of3d_host.hip wxy_tile_fits).  Geometry only (fp64, 8 x 1024 planes: 0.5 / 4 GiB per tile)."""
+    from opticalflow3d_dev_amd import _lib, make_taps
+
+    with env(OF3D_WXY_TILE=1, OF3D_K34_TUNE=0):
+        plan = _lib.Plan(3, nz, 8, 1024, make_taps(2, 2, 5), device=0)
+        try:
+            geo = plan.geometry()
+        finally:
+            plan.close()
+    span = geo["k34"]["s_max"] * 1024 * geo["cap_planes"] * 8
+    assert (span <= 0x7FFFFFFF) == tiled, geo
+    assert (geo["wxy_zt"] > 0) == tiled, geo

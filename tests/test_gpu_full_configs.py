@@ -132,15 +132,18 @@ C5 = (512, 2048, 2048)
 
 
 def test_c5_full_volume_fp32_vs_oracle():
-    """configs[4] (fp32 path) as one volume on one GPU (~250 GB resident; the plan bench --config
-    c5 times): K12's two 256-plane marches, K5c's 64-plane chunks, the packed K34's column
-    blocks at nx 2048; a plain series (one K0 per window: the ring of 14 frames fits beside the
-    workspace), two windows."""
-    sb = _slab(C5, fp32=True, seed=20260206 + 5, k0_batch=0, pipeline=False)
+    """configs[4] (fp32 path) as one volume on one GPU (~265 GB resident; the plan and the series
+    mode bench --config c5 times): K12's two 256-plane marches, K5c's 64-plane chunks, the packed
+    K34's column blocks at nx 2048, and the bench's K0 batching — a ring of 18 frames (the 13-frame
+    window, 4 lookahead frames, one free slot) beside the 155 GB workspace; the first step runs the
+    batched K0 for five windows, the second takes its dt0 from a slot (its outputs are checked)."""
+    sb = _slab(C5, fp32=True, seed=20260206 + 5, k0_batch=5, pipeline=True)
     try:
         _run_steps(sb, 2)
         ks = sb.plan.kernels()
-        assert {"k_grad_xyz_c", "k_wz_solve_c"} <= set(ks), ks
+        assert {"k_tderiv_multi", "k_grad_xyz_c", "k_wz_solve_c"} <= set(ks), ks
+        geo = sb.plan.geometry()
+        assert geo["k0_batch"] == 5 and geo["k12"]["march"] == 256, geo
         assert any(k.startswith("k_prod_wyx") for k in ks), ks
         for box in ((248, 264, 1016, 1032, 1016, 1032),  # K12 march seam (plane 256), x ~ 1024
                     (56, 72, 200, 216, 504, 520),          # K5c chunk 64, x ~ 512
@@ -168,3 +171,95 @@ def test_c5_zslab_rank3_of8_fp32_vs_oracle():
         sb.close()
         del sb
         _free()
+
+
+# ---- configs[1] at its full size through the bench's series plan (round 6) ----
+
+C2 = dict(nz=64, ny=256, nx=256, s=2, t=2, w=5)
+
+
+def test_c2_full_volume_bench_plan_vs_oracle():
+    """configs[1] (13 x 64 x 256 x 256, xyzSig 2, tSig 2, wSig 5, fp64) as bench.py --config c2 runs
+    it: a series of 17 resident frames through one plan with K0 batching (of3d_plan_execute_ahead),
+    the first step forming five windows' dt0, the second using its slot.  The plan's cost model
+    picks 32-plane K12 marches at this size (one round of 256 blocks: csrc/of3d_host.hip, the K12
+    march-length model) — asserted through of3d_plan_geometry — so the crops straddle K12's march
+    seam at plane 32, the column-block seams of the K34 shape the autotune kept, and two corners;
+    then every K34 candidate gives the default plan's bits at this size."""
+    import torch
+
+    import bench
+    from opticalflow3d_dev_amd import _lib, make_taps, radii
+    from conftest import assert_rel_within, bits_equal, oracle3d
+
+    _free()
+    p = C2
+    s, t, w = p["s"], p["t"], p["w"]
+    nz, ny, nx = p["nz"], p["ny"], p["nx"]
+    rd, _, rt, rw = radii(s, t, w)
+    nwin, kb = 2 * rt + 1, 5
+    dev = torch.device("cuda", 0)
+    d_in = bench.synthetic_slab(nwin + kb - 1, nz, ny, nx, 0, nz, 20260206 + 2, dev)
+    vox = nz * ny * nx
+    outs = [torch.full((vox,), float("nan"), dtype=torch.float64, device=dev) for _ in range(3)]
+    outs.append(torch.full((vox,), float("nan"), dtype=torch.float32, device=dev))
+    ptrs = [d_in[i].data_ptr() for i in range(nwin + kb - 1)]
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def run(plan, j):
+        plan.execute(ptrs[j:j + nwin], _lib.OF3D_U16, 0, 0, nz, *[o.data_ptr() for o in outs], stream,
+                     ahead_ptrs=ptrs[j + nwin:])
+
+    plan = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=0, timing=4)
+    try:
+        run(plan, 0)
+        geo0 = plan.geometry()
+        run(plan, 1)
+        torch.cuda.synchronize(dev)
+        ks = set(plan.kernels())
+        geo = plan.geometry()
+    finally:
+        plan.close()
+    assert {"k_tderiv_multi", "k_grad_xyz_c", "k_wz_solve_c"} <= ks, ks
+    assert geo0["k0_batch"] == kb, geo0
+    assert geo["k12"]["march"] == 32 and geo["k12"]["grid"][1] == 2, geo
+    tx = geo["k34"]["tx"]
+    host = d_in[1:1 + nwin].cpu().numpy().view(np.uint16)  # window 1 (its dt0 from the batch's slot)
+    got = [o.view(nz, ny, nx) for o in outs]
+    xs = [min(max(tx - 8, 0), nx - 16)] if geo["k34"]["nbx"] > 1 else [nx // 2 - 8]
+    crops = [(24, 40, 120, 136, xs[0], xs[0] + 16),   # K12 march seam (plane 32) x a K34 column seam
+             (28, 36, 0, 16, 100, 130),             # march seam at the y = 0 edge
+             (0, 16, 0, 16, 0, 16),                 # corner at the origin
+             (48, 64, 240, 256, 236, 256)]          # far corner
+    h = rd + rw
+    for box in crops:
+        z0, z1, y0, y1, x0, x1 = box
+        lo = [max(a - h, 0) for a in (z0, y0, x0)]
+        hi = [min(b + h, n) for b, n in zip((z1, y1, x1), (nz, ny, nx))]
+        sub = np.ascontiguousarray(host[:, lo[0]:hi[0], lo[1]:hi[1], lo[2]:hi[2]])
+        vx, vy, vz, lmin, lmax = oracle3d(sub, s, t, w)
+        sl = (slice(z0 - lo[0], z1 - lo[0]), slice(y0 - lo[1], y1 - lo[1]), slice(x0 - lo[2], x1 - lo[2]))
+        for g, want, name in zip(got[:3], (vx[sl], vy[sl], vz[sl]), ("vx", "vy", "vz")):
+            assert bits_equal(g[z0:z1, y0:y1, x0:x1].cpu().numpy(), want), (box, name)
+        assert_rel_within(got[3][z0:z1, y0:y1, x0:x1].cpu().numpy(), lmin[sl], lmax[sl], 1e-6)
+    # every K34 candidate at this size (plain execute of window 1), bit-identical to the above
+    ref = [o.clone() for o in outs]
+    ncand = geo["k34"]["candidates"]
+    assert ncand >= 2, geo
+    import os
+    for i in range(ncand):
+        os.environ["OF3D_K34_CAND"] = str(i)
+        try:
+            pl = _lib.Plan(3, nz, ny, nx, make_taps(s, t, w), device=0)
+            try:
+                pl.execute(ptrs[1:1 + nwin], _lib.OF3D_U16, 0, 0, nz, *[o.data_ptr() for o in outs], stream)
+                torch.cuda.synchronize(dev)
+            finally:
+                pl.close()
+        finally:
+            del os.environ["OF3D_K34_CAND"]
+        for a, b in zip(ref, outs):
+            it = torch.int64 if a.element_size() == 8 else torch.int32
+            assert bool(torch.equal(a.view(it), b.view(it))), i
+    del d_in, outs, ref
+    _free()
