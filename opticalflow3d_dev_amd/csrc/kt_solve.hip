@@ -10,7 +10,13 @@ namespace of3dk {
 template <typename F, typename RelT>
 const void* k5c_fn(int rw, int nb, int r, int nw, int rt0) {
     if (rt0 > 0) {
-        if (r != 8 || nw != 4) return nullptr;
+        if (nw != 4 || (r != 8 && r != 4)) return nullptr;
+        if (r == 4) {  // 32-plane blocks (three per CU, three window buffers): cache-resident workspaces
+            if (nb != 3) return nullptr;
+            if (rw == 21 && rt0 == 9) return (const void*)k_wz_solve_c<F, RelT, 21, 3, 4, 4, 9>;
+            if (rw == 15 && rt0 == 6) return (const void*)k_wz_solve_c<F, RelT, 15, 3, 4, 4, 6>;
+            return nullptr;
+        }
         if (rw == 21 && rt0 == 9)
             return nb == 3 ? (const void*)k_wz_solve_c<F, RelT, 21, 3, 8, 4, 9> : (const void*)k_wz_solve_c<F, RelT, 21, 2, 8, 4, 9>;
         if (rw == 15 && rt0 == 6)

@@ -1187,12 +1187,29 @@ __global__ __launch_bounds__(1024) void k_prod_wyx_ws(const F* __restrict__ G, F
         constexpr int RPW = S < 8 ? S : 8, SPW = 64 / RPW;
         constexpr int RG = S / RPW;
         const int nsgw = (nseg + SPW - 1) / SPW;
+        // 7 consumer waves (9 producers): a tile whose item groups are one more than whole rounds
+        // of 7 (a 512-wide row at 4 or 8 rows: 8 groups) would make ONE wave run that group as a
+        // second round (its SIMD then carries ~17 % more VALU work per tile than the others); that
+        // group's 256 outputs go instead as single outputs to the first 4 consumer waves, one per
+        // lane, which spreads them over 4 SIMDs (same arithmetic per output: bit-identical)
+        constexpr int NCW = NCT / 64, COLS = SPW * RB;
+        const int ngrp = RG * nsgw;
+        const bool spread = NPW != 8 && RG == 1 && ngrp % NCW == 1;
+        const int nmain = spread ? ngrp - 1 : ngrp;
         for (int tt = 0; tt < ntiles; ++tt) {
             lds_barrier();  // tile tt written
             const F* tile = sw + (tt & 1) * k34_tile(S, cwp);
             const int yb = y0 + tt * S, nr = min(S, nrows - tt * S);
             const auto rq_ = wxy_rsrc(Qp, zl, yb, ny, nx, zt);
-            for (int i = tb; i < 64 * RG * nsgw; i += NCT) {
+            if (spread && tb < RPW * COLS) {  // the leftover group: row tb / COLS, one column per lane
+                const int r = tb / COLS, c0 = (ngrp - 1) * COLS + tb % COLS;
+                if (c0 < txu) {
+                    F o1[1];
+                    lds_pass_c<1, RW, DB>(tile + k34_row(r, cwp), 1, RW + c0, h, o1);
+                    if (r < nr) buf_st<F>(o1[0], rq_, wxy_off<F>(wm, r, xo0 + c0), 0);
+                }
+            }
+            for (int i = tb; i < 64 * nmain; i += NCT) {
                 const int l = i & 63, wg = i >> 6;
                 const int r = (wg % RG) * RPW + ((l >> 2) & 3) + (S >= 8 ? 4 * (l >> 5) : 0);
                 const int sg = (wg / RG) * SPW + (l & 3) + 4 * ((l >> 4) & 1) + (S >= 8 ? 0 : 8 * (l >> 5));
@@ -2365,7 +2382,13 @@ __global__ __launch_bounds__(64 * K5_G) void k_wz_solve_dma(const F* __restrict_
     k5_solve_store<F, RelT, K5_R>(acc, zc0 + g * K5_R - zo0, nzo, (size_t)y * nx + x, ps, vx, vy, vz, rel);
 }
 
-constexpr int K5C_G = 4;  // voxels per straight-line group in K5c's epilogue (k5_solve_store)
+// voxels per straight-line group in K5c's epilogue (k5_solve_store): 4 in fp64 (206 VGPRs either
+// way, set by the nine fields' accumulators); 1 in fp32, where the four voxels' fp64 epilogue state
+// took the kernel from 112 to 158 VGPRs, 4 -> 3 waves per SIMD — the round-4/5 c5 regression (same
+// box, round-3 tree vs round-6: K5c 35.1 vs 36.6 ms, profiles/r06/ab_c5_r03/; G 1 vs 4 on one box:
+// K5c 35.3 / 35.2 vs 36.6 / 36.7 ms, frame 102.8 / 102.9 vs 104.0 / 104.4, profiles/r06/ab6/c5_*)
+template <typename F>
+constexpr int K5C_G = sizeof(F) == 8 ? 4 : 1;
 // LDS-read distance of K5c's W z passes (lds_pass_c's D: window values read D taps ahead).  fp64:
 // 3 (c3 K5c 0.993 / 0.994 -> 0.979 / 0.974 ms over four same-box pairs, c4 6.80 -> 6.75; 4: c3
 // 0.98, c4 slower; the VGPR count stays 206, set by the epilogue); fp32 keeps 2 (c5: 36.0 vs
@@ -2490,7 +2513,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : (R == 8 ? 2 : 3)) void k_wz_
         for (int i = 0; i < R; ++i) asm volatile("" : "+v"(acc[f][i]));
     }
     if (x < nx)
-        k5_solve_store<F, RelT, R, K5C_G>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
+        k5_solve_store<F, RelT, R, K5C_G<F>>(acc, zc0 + gz * R - zo0, nzo, (size_t)kb.by * nx + x, (size_t)gridDim.y * nx, vx,
                                    vy, vz, rel);
     if constexpr (RT0 > 0) {  // the next frame's dt0: the held groups, then any rest of [k0g0, k0g1)
 #pragma unroll

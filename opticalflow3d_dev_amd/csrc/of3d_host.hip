@@ -70,7 +70,7 @@ struct Knobs {
     bool k34_strict = false;  // OF3D_K34_CAND_STRICT=1: a pin past the candidates fails
     bool k34_tune = true;     // OF3D_K34_TUNE=0: the heuristic pick, untimed
     bool k5c = true;      // OF3D_K5C=0: k_wz_solve_dma / k_wz_solve instead of K5c
-    int k5c_r = 8;        // OF3D_K5C_R=4: 32-plane K5c blocks
+    int k5c_r = 0;        // OF3D_K5C_R=4 / 8: 32- / 64-plane K5c blocks (0: by workspace size)
     int k5c_nw = 4;       // OF3D_K5C_NW=8: 8-wave, 128-plane K5c blocks
     int wxy_tile = -1;    // OF3D_WXY_TILE=0 / 1: the W-xy hand-off in plain planes / z-tiled (-1: by size)
     bool pipe = true;     // OF3D_PIPE=0: no next-frame K0 inside K5c
@@ -96,7 +96,8 @@ struct Knobs {
         k.k34_strict = iv("OF3D_K34_CAND_STRICT", 0) == 1;
         k.k34_tune = iv("OF3D_K34_TUNE", 1) != 0;
         k.k5c = iv("OF3D_K5C", 1) != 0;
-        k.k5c_r = iv("OF3D_K5C_R", 8) == 4 ? 4 : 8;
+        k.k5c_r = (int)iv("OF3D_K5C_R", 0);
+        k.k5c_r = k.k5c_r == 4 ? 4 : (k.k5c_r == 8 ? 8 : 0);
         k.k5c_nw = iv("OF3D_K5C_NW", 4) == 8 ? 8 : 4;
         k.wxy_tile = (int)iv("OF3D_WXY_TILE", -1);
         k.pipe = iv("OF3D_PIPE", 1) != 0;
@@ -432,7 +433,12 @@ int k5c_setup(of3d_plan* p) {
     // 39.7 ms), so did 6 planes (48-plane blocks, three per CU: c3 K5c 1.00 -> 1.05 ms,
     // profiles/r04/ab_k5r6/) and the packed-fp32 K5c (float2 lanes: c5 36.5 vs 34.5 ms, round 4,
     // profiles/r04/ab_k5c_fp32/; removed in round 5)
+    // by size (OF3D_K5C_R unset): 32-plane blocks (three per CU) where the nine W-xy fields mostly sit
+    // in the 256 MB Infinity Cache, so the window's 1.94x re-read costs little and the third block
+    // per CU pays: c2 (302 MB) K5c 0.109 / 0.109 vs 0.118 / 0.115 ms, frame 0.379 / 0.378 vs
+    // 0.388 / 0.381 (profiles/r05/ab_c2_k5c_r4/); 64-plane blocks for every larger workspace
     int r = p->kn.k5c_r;
+    if (r == 0) r = (size_t)9 * p->cap_planes * p->ny * p->nx * sizeof(F) <= ((size_t)320 << 20) ? 4 : 8;
     // OF3D_K5C_NW=8: 8-wave blocks of 128 output planes (window 1.33x the outputs instead of
     // 1.66x; one block per CU) — bit-identical but measured no faster (c3 1.118 vs 1.121 ms,
     // c4 8.54 vs 7.90, c5 fp32 43.6 vs 40.4): K5c is not bound by its window re-reads

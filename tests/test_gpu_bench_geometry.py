@@ -207,7 +207,7 @@ def test_c3_fp32_plans_vs_oracle_and_candidates(c3):
 
 
 @pytest.mark.parametrize("variant", [dict(), dict(OF3D_K5C_NW=8), dict(OF3D_K34_UQ=0), dict(OF3D_K34_UQ=2),
-                                     dict(OF3D_K12=1), dict(OF3D_WXY_TILE=0)])
+                                     dict(OF3D_K12=1), dict(OF3D_WXY_TILE=0), dict(OF3D_K5C_R=8)])
 def test_more_than_64_planes_small_xy_vs_oracle(variant):
     """13 x 200 x 41 x 48 (sigma 2, tau 2, omega 5): four K5c z chunks, and a block grid whose
     size is not a multiple of 8 z-chunk sets, so the XCD remap's tail branch runs
