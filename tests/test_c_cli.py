@@ -56,6 +56,12 @@ def test_cli_rejects_bad_taps_header_and_pipes(cli, tmp_path):
     assert r.returncode == 2 and b"bad input files" in r.stderr
     r = subprocess.run([cli, str(img), "7", "0", "8", "8", str(tp), str(tmp_path / "o_")], capture_output=True, text=True)
     assert r.returncode == 2 and "bad dimensions" in r.stderr
+    # a frame count that does not match the file, including one whose byte count nt * nz * ny * nx
+    # * 2 would overflow int64 and wrap: the size is compared as a quotient
+    for nt in ("6", "8", str(2 ** 62 + 7), str(2 ** 63 - 1)):
+        r = subprocess.run([cli, str(img), nt, "2", "8", "8", str(good), str(tmp_path / "o_")],
+                           capture_output=True, text=True)
+        assert r.returncode == 2 and "bad input files" in r.stderr, (nt, r.stderr)
 
 
 def _taps_file(path, s, t, w):
