@@ -356,3 +356,23 @@ def test_wxy_tiled_layout_size_guard(nz, tiled):
     span = geo["k34"]["s_max"] * 1024 * geo["cap_planes"] * 8
     assert (span <= 0x7FFFFFFF) == tiled, geo
     assert (geo["wxy_zt"] > 0) == tiled, geo
+
+
+@pytest.mark.parametrize("shape,knob,r", [((64, 256, 256), None, 4), ((128, 512, 512), None, 8),
+                                          ((64, 256, 256), 8, 8), ((128, 512, 512), 4, 4)])
+def test_k5c_block_rule_by_workspace(shape, knob, r):
+    """K5c takes 32-plane blocks (R 4, three per CU) where the nine fp64 W-xy fields fit 320 MB —
+    configs[1]: 302 MB, cache-resident — and 64-plane blocks (R 8) above (configs[2]: 2.4 GB);
+    OF3D_K5C_R forces either (csrc/of3d_host.hip k5c_setup; geometry only)."""
+    from opticalflow3d_dev_amd import _lib, make_taps
+
+    kv = dict(OF3D_K34_TUNE=0)
+    if knob:
+        kv["OF3D_K5C_R"] = knob
+    with env(**kv):
+        plan = _lib.Plan(3, *shape, make_taps(2, 2, 5), device=0)
+        try:
+            geo = plan.geometry()
+        finally:
+            plan.close()
+    assert geo["k5c"]["r"] == r and geo["k5c"]["nw"] == 4, geo
