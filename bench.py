@@ -174,6 +174,7 @@ def run_2d(args, world, rank, dev):
     if world > 1:
         (elapsed,) = max_over_ranks([elapsed], dev)
     kernels = set(plan.kernels())
+    geometry = plan.geometry()
     plan.close()
     # the same series one output frame per execute (a 1-plane plan, window j)
     plan1 = _lib.Plan(2, 1, ny, nx, make_taps(s, t, w), device=dev.index)
@@ -236,7 +237,7 @@ def run_2d(args, world, rank, dev):
                    "parallelism": f"series replicas x{world}" if world > 1 else "single GPU",
                    "inputs": f"a series of {nt} uint16 frames resident in HBM; one step = its {nout} output "
                              f"frames as one batch (a 2D plan of {nout} planes)",
-                   "frames_per_step": nout, "kernels": sorted(kernels)},
+                   "frames_per_step": nout, "kernels": sorted(kernels), "geometry": geometry},
         "roofline": roof, "cpu_baseline": cpu, "parity_sample": parity, "build": build_stamp(),
         "single_frame": {"ms_per_frame": round(ms1, 5), "value": round(world * plane_b / (ms1 * 1e-3) / 1e6, 3),
                          "unit": "Mvoxels/s", "what": "the same series one output frame per execute (a 1-plane plan)"},
@@ -948,6 +949,7 @@ def run_slab(args, world, rank, local_rank, dev):
                                     f"of the newest frame's {rd + rw} halo {'planes' if axis == 0 else 'rows'} per "
                                     "neighbour, on its own stream beside the previous step's compute"}
     kernels = set(plan.kernels())
+    geometry = plan.geometry()
     own, ai0, ai1, a0, a1, describe = sb.own, sb.ai0, sb.ai1, sb.a0, sb.a1, sb.describe()
     rows_direct = sb.rows_direct
     sb.close()
@@ -1003,7 +1005,7 @@ def run_slab(args, world, rank, local_rank, dev):
                                        f"{split} x{world}, halo {rd + rw}" if world > 1 else "single GPU (whole frame)"),
                        "inputs": f"own part (+ halo) of a ring of {nres} uint16 frames resident in HBM; per step the "
                                  "newest frame's halo exchange (RCCL P2P, own stream) + compute",
-                       "outputs_finite": finite,
+                       "outputs_finite": finite, "geometry": geometry,
                        "row_outputs": "own rows only (of3d_plan_set_rows)" if (axis == 1 and rows_direct) else None,
                        "series": (f"K0 batching: {kb} windows per K0 pass (of3d_plan_execute_ahead)") if kb >= 2 else
                                  ("frame pipelining (of3d_plan_execute_next)" if not args.no_pipeline else "plain")},
@@ -1204,6 +1206,7 @@ def main():
     # sanity: finite outputs
     finite = bool(torch.isfinite(d_vx).all().item())
     kernels = set(plan.kernels())
+    geometry = plan.geometry()
     ms_step = elapsed / args.steps * 1e3
     parity = None
     if rank == 0 and not args.no_parity_sample:
@@ -1268,7 +1271,7 @@ def main():
                        "inputs": (f"a time series of {nres} uint16 frames resident in HBM: {kb} consecutive "
                                   f"{nwin}-frame windows (output frames), step i computes window i mod {kb}"
                                   if kb else f"one {nwin}-frame window of uint16 frames resident in HBM"),
-                       "outputs_finite": finite,
+                       "outputs_finite": finite, "geometry": geometry,
                        "frame_pipelining": ("each step's W-z/solve kernel also forms the next step's temporal "
                                             "derivative (of3d_plan_execute_next); stage grad_xy is then empty")
                        if pipe else None,
