@@ -10,8 +10,8 @@ template <typename F> const void* k0_kernel_dt(int dtype);                   // 
 template <typename F> const void* k0c_fn(int dtype, int rt);                 // kt_grad.hip
 template <typename F> const void* k0m_fn(int dtype, int rt, int m);          // kt_grad.hip (K0 batching)
 template <typename F> const void* k1c_fn(int dtype, int rd, int rs);         // kt_grad.hip
-template <typename F> const void* k12_fn(int dtype, int rd, int rs);         // kt_grad3.hip (fused y/x/z gradients)
-template <typename F> size_t k12_lds(int dtype, int rd);                     // kt_grad3.hip
+template <typename F> const void* k12_fn(int dtype, int rd, int rs, bool deep = false);         // kt_grad3.hip (fused y/x/z gradients)
+template <typename F> size_t k12_lds(int dtype, int rd, bool deep = false);                     // kt_grad3.hip
 template <typename F> const void* k3_kernel(int np, int rw);                 // kt_prod_legacy.hip
 template <typename F> const void* k4_kernel(int nf, int rw);                 // kt_prod_legacy.hip
 template <typename F, int NP> const void* k34_fn(int rw, int s, int rb);     // kt_prod.hip

@@ -1715,8 +1715,17 @@ __host__ __device__ constexpr int k12_slot_bytes() { return ((k12_slot_granules<
 // b128 groups).
 template <typename F>
 __host__ __device__ constexpr int k12_ap() { return k12_cw<F>() + 4; }
+// fp64 (round 6): ONE copy per A row; the x windows read single 8-byte elements (ds_read_b64:
+// 2 LDS cycles per 512 B, the b128 rate; kept from pairing into ds_read2_b64 by empty fences) —
+// half the y-pass LDS writes and half the A-tile bytes, which buys the third DMA slot below.
+// fp32 keeps the odd-shifted copies (its 4-byte reads would run at half rate).
+constexpr bool k12_odd_fp64 = false;
 template <typename F>
-__host__ __device__ constexpr int k12_a_bytes() { return 2 * 3 * 2 * K12_TY * k12_ap<F>() * (int)sizeof(F); }
+__host__ __device__ constexpr bool k12_odd() { return sizeof(F) == 4 || k12_odd_fp64; }
+template <typename F>
+__host__ __device__ constexpr int k12_a_bytes() {
+    return 2 * 3 * (k12_odd<F>() ? 2 : 1) * K12_TY * k12_ap<F>() * (int)sizeof(F);
+}
 // planes per DMA chunk: 2 where two chunks of slots + the A tiles fit 80 KiB and the
 // kernel's registers allow 4 waves per SIMD (fp32 rd 3 / 6: two 8-wave blocks per CU),
 // else 3 where they fit 160 KiB, else 2
@@ -1727,12 +1736,23 @@ __host__ __device__ constexpr int k12_k() {
     if (6 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024) return 3;
     return 4 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024 ? 2 : 1;
 }
-template <typename T, typename F, int RD>
+// chunks of DMA slots: DEEP instances 3 (each plane's loads get two steps to land) for one-plane
+// chunks of the non-deferred (fp64) kernel where three slots fit beside the A tiles, else 2 (one
+// step).  The host takes DEEP for marches of >= 128 planes: same box, c4 (256-plane marches) K12
+// 3.19 -> 3.10 ms; c3 (64) equal; c2 (32) 0.088 -> 0.091 (profiles/r06/abk12/)
+template <typename T, typename F, int RD, bool DEEP>
+__host__ __device__ constexpr int k12_nch() {
+    return DEEP && !k12_defer<F>() && k12_k<T, F, RD>() == 1 &&
+                   3 * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>() <= 160 * 1024
+               ? 3
+               : 2;
+}
+template <typename T, typename F, int RD, bool DEEP = false>
 __host__ __device__ constexpr int k12_lds_bytes() {
-    return 2 * k12_k<T, F, RD>() * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>();
+    return k12_nch<T, F, RD, DEEP>() * k12_k<T, F, RD>() * k12_slot_bytes<T, F, RD>() + k12_a_bytes<F>();
 }
 
-template <typename T, typename F, int RD, int RS>
+template <typename T, typename F, int RD, int RS, bool DEEP = false>
 __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __restrict__ Ic, const F* __restrict__ D0,
                                                              int zin0, int nzc, int ny, int nx, DevTaps<F> tp,
                                                              F* __restrict__ G, size_t fs, int zg0, int q0, int nq,
@@ -1740,15 +1760,18 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
     constexpr int TY = K12_TY, TX = k12_tx<F, RD>(), NRW = TY + 2 * RD, CW = k12_cw<F>();
     constexpr int NWX = k12_nwx<F>(), NWV = NWX * TY;  // waves per row; per block
     constexpr int NR = 2 * RD + 2, NRS = RD + 1, AP = k12_ap<F>();  // ring slots; A tile pitch
-    constexpr int AF = 2 * TY * AP, AB = 3 * AF;  // A field stride (even + odd copy), buffer stride
+    constexpr bool ODD = k12_odd<F>();
+    constexpr int AF = (ODD ? 2 : 1) * TY * AP, AB = 3 * AF;  // A field stride (even [+ odd] copy), buffer stride
     static_assert(NRS >= 2 * RS + 1 && NR % NRS == 0 && NR % 2 == 0 && TX >= 8, "K12 geometry");
     constexpr int EF = 16 / (int)sizeof(F), ET = 16 / (int)sizeof(T);  // elements per granule
     constexpr int GD = CW / EF + 1, GI = CW / ET + 1;                   // granules per staged row
     constexpr int NG = NRW * (GD + GI), NJ = (NG + 63) / 64;            // granules / DMA instrs per plane
     constexpr int K = k12_k<T, F, RD>();  // planes per DMA chunk
-    constexpr int SLOT = k12_slot_bytes<T, F, RD>(), NSLOT = 2 * K;
-    static_assert(k12_lds_bytes<T, F, RD>() <= 160 * 1024, "K12 LDS");
+    constexpr int NCH = k12_nch<T, F, RD, DEEP>();  // chunks of slots (DMA issued NCH - 1 chunks ahead)
+    constexpr int SLOT = k12_slot_bytes<T, F, RD>(), NSLOT = NCH * K;
+    static_assert(k12_lds_bytes<T, F, RD, DEEP>() <= 160 * 1024, "K12 LDS");
     constexpr int NJW = (NJ + NWV - 1) / NWV;                           // DMA instrs per wave per plane
+    constexpr int NJMIN = NJ / NWV;  // ... on the waves with the fewest (NJW - 1 or NJW)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
     F* At = reinterpret_cast<F*>(smem_raw + NSLOT * SLOT);  // [2 buffers][3 fields][even, odd][TY][AP]
     const int t = threadIdx.x, lane = t & 63;
@@ -1843,7 +1866,7 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                 a[r * AP] = o;
                 // odd copy at c - 1; lane c = 0 writes the pad column AP - 1 of the row before
                 // (even copy's last row for r = 0), which no window reads: no exec mask
-                a[TY * AP + r * AP - 1] = o;
+                if constexpr (ODD) a[TY * AP + r * AP - 1] = o;
             }
         };
         if (role == 0)
@@ -1872,10 +1895,11 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                 o1 = o1 + (r1[slotz(cz - k, NR)] + r1[slotz(cz + k, NR)]) * hg[k];
                 o4 = o4 + (r4[slotz(cz - k, NR)] - r4[slotz(cz + k, NR)]) * hd[k];
             }
-            if (st_ok) {
+            if (NCH == 3 || st_ok) {  // NCH 3: every lane stores (vmcnt counts), others out of range
                 const size_t pq = (size_t)(q - zg0) * plane;
-                buf_st<F>(o1, buf_rsrc(G + pq), vout, sout);
-                buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vout, sout);
+                const unsigned vo = NCH == 3 && !st_ok ? 0x80000000u : vout;
+                buf_st<F>(o1, buf_rsrc(G + pq), vo, sout);
+                buf_st<F>(o4, buf_rsrc(G + 3 * fs + pq), vo, sout);
             }
         }
         if (s >= RD + RS && s < nout + RD + RS) {  // plane q = qa + s - RD - RS: dy and dx
@@ -1887,16 +1911,34 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                 o2 = o2 + (r2[slotz(cz - k, NRS)] + r2[slotz(cz + k, NRS)]) * hs[k];
                 o3 = o3 + (r3[slotz(cz - k, NRS)] + r3[slotz(cz + k, NRS)]) * hs[k];
             }
-            if (st_ok) {
+            if (NCH == 3 || st_ok) {
                 const size_t pq = (size_t)(q - zg0) * plane;
-                buf_st<F>(o2, buf_rsrc(G + fs + pq), vout, sout);
-                buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vout, sout);
+                const unsigned vo = NCH == 3 && !st_ok ? 0x80000000u : vout;
+                buf_st<F>(o2, buf_rsrc(G + fs + pq), vo, sout);
+                buf_st<F>(o3, buf_rsrc(G + 2 * fs + pq), vo, sout);
             }
         }
     };
+    // NCH 3 (one-plane chunks): at step s plane s + 1 must have landed.  Issued at step s - 2
+    // (right after that step's barrier); behind it this wave issued the stores of steps s - 2 and
+    // s - 1 (unconditional: zst of them) and plane s + 2's loads (>= NJMIN): wait until at most
+    // that many are left, rounded down to a few immediates (a smaller count only waits longer)
+    auto zst = [&](int q) { return (q >= 2 * RD ? 2 : 0) + (q >= RD + RS && q < nout + RD + RS ? 2 : 0); };
+    auto wait_plane = [&](int s) {
+        const int cnt = zst(s - 2) + zst(s - 1) + (s + 2 < nsteps ? NJMIN : 0);
+        if (cnt >= 8 + NJMIN)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + NJMIN) : "memory");
+        else if (cnt >= 4 + NJMIN)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + NJMIN) : "memory");
+        else if (cnt >= NJMIN)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NJMIN) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
     issue_chunk(0);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    issue_chunk(1);
+#pragma unroll
+    for (int m = 1; m < NCH; ++m) issue_chunk(m);  // (clamped to nsteps)
     ypass_step(0, 0);
     for (int u0 = 0; u0 < nsteps; u0 += NR) {
         bool done = false;
@@ -1907,10 +1949,15 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                     constexpr int j = J;
                     const int s = u0 + j;
                     const bool chunk_end = s % K == K - 1;
-                    if (chunk_end) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (chunk_end) {
+                        if constexpr (NCH == 3)
+                            wait_plane(s);
+                        else
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
                     lds_barrier();
                     if (chunk_end) {
-                        const int m2 = s / K + 2;
+                        const int m2 = s / K + NCH;
                         if (m2 * K < nsteps) issue_chunk(m2);
                     }
                     // k12_defer: the z passes of step s - 1 here, ahead of this step's x-window
@@ -1924,6 +1971,15 @@ __global__ __launch_bounds__(k12_threads<F>()) void k_grad_xyz_c(const T* __rest
                     const F* arow = At + (j & 1) * AB + role * AP;  // NR even: parity of s
                     auto window = [&]<int R>(int f, F (&x)[2 * R + 2]) {
                         const int st = cx - R;
+                        if constexpr (!ODD) {  // single elements, one ds_read_b64 each
+                            const F* q = arow + f * AF + st;
+#pragma unroll
+                            for (int i = 0; i <= 2 * R; ++i) {
+                                x[i] = q[i];
+                                asm volatile("" ::: "memory");  // no pairing into ds_read2_b64
+                            }
+                            return;
+                        }
                         const F* q = arow + f * AF + ((st & 1) ? TY * AP + st - 1 : st);
                         typedef F F2 __attribute__((ext_vector_type(2)));
                         const F2* q2 = reinterpret_cast<const F2*>(__builtin_assume_aligned(q, 2 * sizeof(F)));

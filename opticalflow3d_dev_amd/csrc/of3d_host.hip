@@ -162,7 +162,7 @@ struct of3d_plan {
     int64_t ya = 0, yb = 0;  // output rows [ya, yb) (of3d_plan_set_rows; default all)
     unsigned used = 0;       // kernel families launched so far (KU_* bits, of3d_plan_kernels)
     // geometry of the last execution (of3d_plan_geometry): K12 march length and grid, K0 windows
-    int last_k12_zc = 0, last_k12_gx = 0, last_k12_gy = 0, last_k0m = 0;
+    int last_k12_zc = 0, last_k12_gx = 0, last_k12_gy = 0, last_k12_deep = 0, last_k0m = 0;
     hipEvent_t ev_done = nullptr;  // recorded on the caller's stream at the end of every execution
     // fused K34 (products + W y + W x); fn == nullptr: separate K3 and K4
     struct K34Geom {
@@ -614,8 +614,10 @@ int set_attrs_t(of3d_plan* p) {
     for (int dt : {OF3D_U8, OF3D_U16, OF3D_F32}) {
         if (const void* f = k1c_fn<F>(dt, p->rd, p->rs))
             OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        if (const void* f = k12_fn<F>(dt, p->rd, p->rs))
-            OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)k12_lds<F>(dt, p->rd)));
+        for (bool deep : {false, true})
+            if (const void* f = k12_fn<F>(dt, p->rd, p->rs, deep))
+                OF3D_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)k12_lds<F>(dt, p->rd, deep)));
     }
     if (k5c_setup<F>(p)) return -1;
     return k34_setup<F>(p, p->ndim == 3 ? 9 : 5);
@@ -1014,13 +1016,17 @@ int run_t(of3d_plan* p, const void* const* d_frames, int dtype, int64_t frame_z0
                 while (zc > 16 && (long)ntile * cdiv(nq, zc) < 1024) zc /= 2;
             }
             const unsigned gx = 8 * cdiv(ntile, 8);
-            const size_t lds = k12_lds<F>(dtype, p->rd);
+            // marches of >= 128 planes: the three-DMA-slot instance (fp64 rd 6; the others have one)
+            const bool deep = zc >= 128;
+            const void* k12x = deep ? k12_fn<F>(dtype, p->rd, p->rs, true) : k12;
+            const size_t lds = k12_lds<F>(dtype, p->rd, deep);
             void* args[] = {(void*)&Ic, (void*)&D0c, (void*)&zin0, (void*)&nzc, (void*)&ny, (void*)&nx, (void*)&tp,
                             (void*)&Go, (void*)&fs, (void*)&zg0, (void*)&qa, (void*)&nq, (void*)&zc, (void*)&ntile,
                             (void*)&nbx};
-            OF3D_HIP(hipLaunchKernel(k12, dim3(gx, cdiv(nq, zc)), dim3(k12_threads<F>()), args, lds, st));
+            OF3D_HIP(hipLaunchKernel(k12x, dim3(gx, cdiv(nq, zc)), dim3(k12_threads<F>()), args, lds, st));
             p->used |= KU_K12;
             p->last_k12_zc = zc, p->last_k12_gx = (int)gx, p->last_k12_gy = (int)cdiv(nq, zc);
+            p->last_k12_deep = k12x != k12;
             return 0;
         }
         const void* k2c = nullptr;
@@ -1712,11 +1718,12 @@ int of3d_plan_geometry(const of3d_plan* p, char* buf, size_t n) {
              "{\"ndim\": %d, \"nz\": %lld, \"ny\": %lld, \"nx\": %lld, \"fp32\": %d, \"general\": %d, "
              "\"cap_planes\": %lld, \"wxy_zt\": %d, \"k34\": {\"cw\": %d, \"s\": %d, \"tx\": %d, \"nbx\": %d, "
              "\"threads\": %d, \"lds\": %zu, \"candidates\": %zu, \"s_max\": %d}, \"k5c\": {\"r\": %d, \"nw\": %d, "
-             "\"lds\": %zu}, \"k12\": {\"march\": %d, \"grid\": [%d, %d]}, \"k0_batch\": %d, \"ncu\": %d}",
+             "\"lds\": %zu}, \"k12\": {\"march\": %d, \"grid\": [%d, %d], \"deep\": %d}, \"k0_batch\": %d, \"ncu\": %d}",
              p->ndim, (long long)p->nz, (long long)p->ny, (long long)p->nx, (int)p->fp32, (int)p->general,
              (long long)p->cap_planes, p->wxy_zt, p->k34.cw, p->k34.s, p->k34.tx, p->k34.nbx,
              p->k34.nthr ? p->k34.nthr : p->k34.cw, p->k34.lds, p->k34_cand.size(), smax, p->k5c ? p->k5c_r : 0,
-             p->k5c ? p->k5c_nw : 0, p->k5c_lds, p->last_k12_zc, p->last_k12_gx, p->last_k12_gy, p->last_k0m, p->ncu);
+             p->k5c ? p->k5c_nw : 0, p->k5c_lds, p->last_k12_zc, p->last_k12_gx, p->last_k12_gy, p->last_k12_deep, p->last_k0m,
+             p->ncu);
     const std::string out(tmp);
     if (buf && n) {
         const size_t k = std::min(n - 1, out.size());

@@ -52,9 +52,9 @@ def env(**kv):
                 os.environ[k] = v
 
 
-def run_plan(d_in, nz, ny, nx, s, t, w, mode=0):
+def run_plan(d_in, nz, ny, nx, s, t, w, mode=0, geo=None):
     """One output frame through a device plan as bench.py runs it: (vx, vy, vz, rel) device
-    tensors and the kernel families the plan launched."""
+    tensors and the kernel families the plan launched (and its of3d_plan_geometry into `geo`)."""
     import torch
 
     from opticalflow3d_dev_amd import _lib, make_taps
@@ -71,6 +71,8 @@ def run_plan(d_in, nz, ny, nx, s, t, w, mode=0):
                      *[o.data_ptr() for o in outs], torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
         kernels = plan.kernels()
+        if geo is not None:
+            geo.append(plan.geometry())
     finally:
         plan.close()
     return [o.view(nz, ny, nx) for o in outs], kernels
@@ -248,15 +250,18 @@ def long_volume():
 @pytest.mark.parametrize("zc", [32, 128, 256])
 def test_k12_long_marches_vs_oracle(long_volume, zc, fp32):
     """OF3D_K12_ZC = 32 / 128 / 256 (the c2 / c4 / c5 marches) against the full oracle: fp64
-    bitwise, fp32 within 1e-4 max|v| and bit-identical to the 16-plane marches of the same plan."""
+    bitwise (marches of >= 128 planes on the three-DMA-slot instance), fp32 within 1e-4 max|v|
+    and bit-identical to the 16-plane marches of the same plan."""
     from opticalflow3d_dev_amd import _lib
 
     d_in, (vx, vy, vz, lmin, lmax) = long_volume
     p = LONG
     mode = _lib.OF3D_FP32 if fp32 else 0
+    geo = []
     with env(OF3D_K12=1, OF3D_K12_ZC=zc):
-        outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode)
+        outs, kernels = run_plan(d_in, p["nz"], p["ny"], p["nx"], p["s"], p["t"], p["w"], mode=mode, geo=geo)
     assert "k_grad_xyz_c" in kernels, kernels
+    assert geo[0]["k12"]["march"] == zc and geo[0]["k12"]["deep"] == int(not fp32 and zc >= 128), geo
     if not fp32:
         for g, want, name in zip(outs[:3], (vx, vy, vz), ("vx", "vy", "vz")):
             assert bits_equal(g.cpu().numpy(), want), (zc, name)

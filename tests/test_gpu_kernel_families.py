@@ -14,7 +14,8 @@ from opticalflow3d_dev_amd import _lib, make_taps, radii
 
 pytestmark = pytest.mark.gpu
 
-FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_NW", "OF3D_K34_UQ", "OF3D_WXY_TILE")
+FAMILY_ENV = ("OF3D_K34", "OF3D_K5C", "OF3D_K1C", "OF3D_K12", "OF3D_K5C_NW", "OF3D_K34_UQ", "OF3D_WXY_TILE",
+              "OF3D_K12_ZC")
 
 
 def _run(img, s, t, w, ndim, mode, old, force=None, kernels=None):
@@ -95,6 +96,24 @@ def test_fused_gradients_k12_forced(case, fp32):
     mode = _lib.OF3D_FP32 if fp32 else 0
     new = _run(img, s, t, w, ndim, mode, old=False, force={"OF3D_K12": "1"})
     ref = _run(img, s, t, w, ndim, mode, old=True)
+    for a, b in zip(new, ref):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
+
+
+@pytest.mark.parametrize("zc", [0, 16, 40])
+@pytest.mark.parametrize("fp32", [False, True])
+def test_fused_gradients_k12_xyzsig1(zc, fp32):
+    """K12 at xyzSig 1 (rd 3, rs 1: three-plane DMA chunks in fp64 since its A tiles hold one
+    copy per row) forced, with whole-volume, 16- and 40-plane marches (chunk tails and march
+    tails), against K1c + K2c and the older kernels: every output bit-identical."""
+    rng = np.random.default_rng(450 + zc)
+    img = rng.integers(0, 4096, size=(13, 45, 70, 232)).astype(np.uint16)  # 16-byte u16 rows
+    mode = _lib.OF3D_FP32 if fp32 else 0
+    force = {"OF3D_K12": "1"} | ({"OF3D_K12_ZC": str(zc)} if zc else {})
+    kernels = []
+    new = _run(img, 1, 2, 5, 3, mode, old=False, force=force, kernels=kernels)
+    assert "k_grad_xyz_c" in kernels, kernels
+    ref = _run(img, 1, 2, 5, 3, mode, old=True)
     for a, b in zip(new, ref):
         assert a.dtype == b.dtype and np.array_equal(a.view(np.uint8), b.view(np.uint8))
 
